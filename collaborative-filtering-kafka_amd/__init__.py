@@ -1,0 +1,7 @@
+"""MI355X-native ALS engine for the Collaborative-Filtering-Kafka hot path.
+
+The directory name contains dashes, so it is loaded under the module name ``cfk_amd`` (see
+``load_package`` in ``__graft_entry__.py``). The native library is ``build/libcfk_als.so``.
+"""
+from .engine import ALSEngine, Dataset, factor_stride, u01, write_prediction_csv  # noqa: F401
+from .app import ALSApp  # noqa: F401

@@ -1,0 +1,125 @@
+"""ALSApp: the reference topology's iteration semantics on 1..G GPUs (one process per GPU).
+
+Reference: apps/ALSApp.java:41-48 (configuration), :115-163 (the unrolled ALS loop),
+processors/UFeatureInitializer.java:36-66 (U0 after the EOF barrier), processors/FeatureCollector.java:72-110.
+
+Bulk-synchronous restatement: U0 -> for i in 0..N-1 { M_i = solve(movies | U_i); U_{i+1} = solve(users | M_i) }.
+The reference fires each entity's solve as soon as its last factor row arrives (MFeatureCalculator.java:65);
+every solve of a half depends only on the previous half's factors, so the results are identical.
+Final output = (U_N, M_{N-1}) as in the reference's movie-features-N / user-features-N topics.
+
+Multi-GPU: entities are sharded by raw id % G (PureModStreamPartitioner.java:9-10 with numPartitions = G,
+equal to (id % P) % G when G divides P). Every rank holds its shard's in-blocks and a full replica of both
+factor matrices in slot order; each half-iteration ends with ONE RCCL all-gather (torch.distributed, backend
+"nccl" = RCCL over xGMI) of the updated shard -- the replacement for the feature topics' block-to-block
+fan-out (ALSApp.java:105-148, README.md:157).
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from .engine import ALSEngine, Dataset, SIDE_MOVIE, SIDE_USER
+
+
+class ALSApp:
+    def __init__(self, num_partitions: int, num_features: int, als_lambda: float, num_als_iterations: int,
+                 num_movies: int | None = None, num_users: int | None = None, *, precision: str = "f32",
+                 seed: int = 42, device: int = 0, rank: int = 0, world_size: int = 1, group=None):
+        self.NUM_PARTITIONS = num_partitions
+        self.NUM_FEATURES = num_features
+        self.ALS_LAMBDA = float(np.float32(als_lambda))     # Float.parseFloat (ALSAppRunner.java:19)
+        self.NUM_ALS_ITERATIONS = num_als_iterations
+        self.NUM_MOVIES = num_movies
+        self.NUM_USERS = num_users
+        self.precision = precision
+        self.seed = seed
+        self.device = device
+        self.rank = rank
+        self.world = world_size
+        self.group = group
+        self.engine = None
+        self.ds = None
+        self.info = [None, None]
+
+    # -------------------------------------------------------------------------------------------------
+    def setup(self, ds: Dataset, check_duplicates: bool = True) -> "ALSApp":
+        """Blocks of this rank's shard + factor replicas + U0 (UFeatureInitializer after the EOF barrier)."""
+        nm, nu, nnz = ds.counts()
+        if self.NUM_MOVIES is not None and (nm, nu) != (self.NUM_MOVIES, self.NUM_USERS):
+            raise ValueError(f"NUM_MOVIES/NUM_USERS = {self.NUM_MOVIES}/{self.NUM_USERS} but the dataset rates "
+                             f"{nm} movies and {nu} users (the reference collector would never fire, "
+                             f"FeatureCollector.java:43)")
+        if check_duplicates and ds.count_duplicates():
+            raise ValueError("duplicate (user, movie) pairs: the reference never completes such an entity "
+                             "(MFeatureCalculator.java:65)")
+        self.ds = ds
+        torch.cuda.set_device(self.device)
+        eng = ALSEngine(self.NUM_FEATURES, self.precision, self.device)
+        eng.use_torch_stream()
+        for side in (SIDE_MOVIE, SIDE_USER):
+            blk = ds.shard_block(side, self.world, self.rank)
+            opp = ds.shard_info(1 - side, self.world, self.rank)
+            eng.alloc_factors(side, blk["n_slots"])
+            eng.set_block(side, blk["row_ptr"], blk["col"], blk["ratings"], blk["row_offset"], opp["n_slots"])
+            self.info[side] = {k: blk[k] for k in ("n_rows", "row_offset", "nnz", "slots_per_shard", "n_slots")}
+        u0 = ds.init_user_factors(self.NUM_FEATURES, self.seed, self.world)
+        eng.write_factors(SIDE_USER, u0)
+        self.engine = eng
+        self.nnz_total = nnz
+        return self
+
+    # -------------------------------------------------------------------------------------------------
+    def _allgather(self, side: int):
+        if self.world == 1:
+            return
+        import torch.distributed as dist
+        S = self.info[side]["slots_per_shard"]
+        full = self.engine.factors[side]
+        dist.all_gather_into_tensor(full, full[self.rank * S:(self.rank + 1) * S], group=self.group)
+
+    def movie_half(self):
+        """MFeatureCalculator-i over this rank's movies + all-gather (movie-features-i topic)."""
+        self.engine.solve_half(SIDE_MOVIE, self.ALS_LAMBDA)
+        self._allgather(SIDE_MOVIE)
+
+    def user_half(self):
+        """UFeatureCalculator-i over this rank's users + all-gather (user-features-(i+1) topic)."""
+        self.engine.solve_half(SIDE_USER, self.ALS_LAMBDA)
+        self._allgather(SIDE_USER)
+
+    def iteration(self):
+        self.movie_half()
+        self.user_half()
+
+    def run(self, iterations: int | None = None) -> float:
+        n = self.NUM_ALS_ITERATIONS if iterations is None else iterations
+        torch.cuda.synchronize(self.device)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            self.iteration()
+        torch.cuda.synchronize(self.device)
+        return time.perf_counter() - t0
+
+    # -------------------------------------------------------------------------------------------------
+    def factors(self):
+        """(U, M) in ascending raw-id order (FeatureCollector.constructFeatureMatrices, :72-88)."""
+        U = self.engine.read_factors(SIDE_USER)
+        M = self.engine.read_factors(SIDE_MOVIE)
+        return U[self.ds.slots(SIDE_USER, self.world)], M[self.ds.slots(SIDE_MOVIE, self.world)]
+
+    def sq_error(self):
+        """Sum of squared errors over all observed ratings (all ranks) and the rating count."""
+        se, cnt = self.engine.sq_error(SIDE_MOVIE)
+        if self.world > 1:
+            import torch.distributed as dist
+            t = torch.tensor([se, float(cnt)], dtype=torch.float64, device=f"cuda:{self.device}")
+            dist.all_reduce(t, group=self.group)
+            se, cnt = float(t[0]), int(t[1])
+        return se, cnt
+
+    def mse(self) -> float:
+        se, cnt = self.sq_error()
+        return se / cnt

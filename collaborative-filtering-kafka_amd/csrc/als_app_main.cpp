@@ -1,0 +1,186 @@
+// als_app -- command-line replacement for ALSAppRunner (apps/ALSAppRunner.java:10-37) on one MI355X.
+//
+//   als_app NUM_PARTITIONS NUM_FEATURES LAMBDA NUM_ITERATIONS dataset NUM_MOVIES NUM_USERS
+//           [--precision f32|f64] [--seed S] [--device D] [--out DIR]
+//
+// Same 7 positional arguments (README.md:35); the extras are optional trailing flags. The run follows the
+// reference topology (ALSApp.java:52-184) bulk-synchronously: ingest (NetflixDataFormatProducer), in-blocks
+// (M/URatings2BlocksProcessor), U0 after the EOF barrier (UFeatureInitializer), N iterations of
+// MFeatureCalculator-i then UFeatureCalculator-i on the GPU, and FeatureCollector's prediction matrix written
+// to ./predictions/prediction_matrix_<timestamp> in EJML dense-CSV layout.
+// Deviations that turn reference hangs into errors: duplicate (user, movie) pairs, and NUM_MOVIES /
+// NUM_USERS not equal to the rated-entity counts (FeatureCollector.java:43 would never fire).
+#include <sys/stat.h>
+#include <sys/time.h>
+
+#include <cerrno>
+#include <climits>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <cmath>
+#include <ctime>
+#include <string>
+#include <vector>
+
+#include "als.h"
+#include "als_host.h"
+
+namespace {
+
+// java.sql.Timestamp.toString() of System.currentTimeMillis(): "yyyy-mm-dd hh:mm:ss.f" (fraction without
+// trailing zeros, at least one digit).
+std::string java_timestamp() {
+    struct timeval tv;
+    gettimeofday(&tv, nullptr);
+    struct tm lt;
+    time_t sec = tv.tv_sec;
+    localtime_r(&sec, &lt);
+    char buf[64];
+    strftime(buf, sizeof(buf), "%Y-%m-%d %H:%M:%S", &lt);
+    char frac[16];
+    snprintf(frac, sizeof(frac), "%03d", (int)(tv.tv_usec / 1000));
+    std::string f(frac);
+    while (f.size() > 1 && f.back() == '0') f.pop_back();
+    return std::string(buf) + "." + f;
+}
+
+bool parse_int(const char* s, long long lo, long long hi, long long& out) {
+    char* end = nullptr;
+    errno = 0;
+    long long v = strtoll(s, &end, 10);
+    if (errno || !end || *end || end == s || v < lo || v > hi) return false;
+    out = v;
+    return true;
+}
+
+int die(const char* what) {
+    fprintf(stderr, "als_app: %s: %s\n", what, als_last_error());
+    return 1;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc - 1 < 7) {   // ALSAppRunner.java:11-14
+        printf("\x1b[31mARGUMENTS MISSING\x1b[0m\n");
+        return 0;
+    }
+    long long P, K, N, NM, NU;
+    if (!parse_int(argv[1], 1, INT_MAX, P) || !parse_int(argv[2], 1, 64, K) || !parse_int(argv[4], 0, INT_MAX, N) ||
+        !parse_int(argv[6], 0, INT_MAX, NM) || !parse_int(argv[7], 0, INT_MAX, NU)) {
+        fprintf(stderr, "als_app: bad integer argument (NUM_FEATURES must be 1..64)\n");
+        return 1;
+    }
+    char* end = nullptr;
+    const float lambda = strtof(argv[3], &end);   // Float.parseFloat (ALSAppRunner.java:19)
+    if (!end || *end) {
+        fprintf(stderr, "als_app: bad LAMBDA\n");
+        return 1;
+    }
+    const char* dataset = argv[5];
+    int precision = ALS_F32;
+    unsigned long long seed = 42;
+    int device = 0;
+    std::string outdir = "./predictions";
+    for (int i = 8; i < argc; ++i) {
+        std::string a = argv[i];
+        if (a == "--precision" && i + 1 < argc) {
+            std::string p = argv[++i];
+            if (p == "f64") precision = ALS_F64;
+            else if (p == "f32") precision = ALS_F32;
+            else { fprintf(stderr, "als_app: --precision f32|f64\n"); return 1; }
+        } else if (a == "--seed" && i + 1 < argc) {
+            seed = strtoull(argv[++i], nullptr, 10);
+        } else if (a == "--device" && i + 1 < argc) {
+            device = atoi(argv[++i]);
+        } else if (a == "--out" && i + 1 < argc) {
+            outdir = argv[++i];
+        } else {
+            fprintf(stderr, "als_app: unknown option %s\n", a.c_str());
+            return 1;
+        }
+    }
+
+    printf("Start at %s\n", java_timestamp().c_str());
+    als_dataset* ds = nullptr;
+    if (als_dataset_load_netflix(dataset, &ds) != ALS_OK) return die("ingest");
+    printf("Producer is done at %s\n", java_timestamp().c_str());
+    int64_t nm, nu, nnz, dups = 0;
+    als_dataset_counts(ds, &nm, &nu, &nnz);
+    if (als_dataset_count_duplicates(ds, &dups) != ALS_OK) return die("duplicates");
+    if (dups > 0) {
+        fprintf(stderr, "als_app: %lld duplicate (user, movie) pairs: the reference topology never completes on such "
+                        "input (MFeatureCalculator.java:65)\n", (long long)dups);
+        return 1;
+    }
+    if (nm != NM || nu != NU) {
+        fprintf(stderr, "als_app: NUM_MOVIES/NUM_USERS = %lld/%lld but the dataset rates %lld movies and %lld users; "
+                        "the reference collector would wait forever (FeatureCollector.java:43)\n",
+                (long long)NM, (long long)NU, (long long)nm, (long long)nu);
+        return 1;
+    }
+    printf("Got EOF: %lld ratings, %lld movies, %lld users (NUM_PARTITIONS=%lld; 1 GPU)\n", (long long)nnz,
+           (long long)nm, (long long)nu, P);
+
+    als_engine* e = nullptr;
+    if (als_engine_create(device, (int)K, precision, &e) != ALS_OK) return die("engine");
+    const int k = (int)K;
+    for (int side = 0; side < 2; ++side) {
+        int64_t n_rows, row_off, bnnz, S, n_slots;
+        als_dataset_shard_info(ds, side, 1, 0, &n_rows, &row_off, &bnnz, &S, &n_slots);
+        std::vector<int64_t> rp(n_rows + 1);
+        std::vector<int32_t> col(bnnz);
+        std::vector<int16_t> rat(bnnz);
+        if (als_dataset_shard_block(ds, side, 1, 0, rp.data(), col.data(), rat.data(), nullptr) != ALS_OK)
+            return die("blocks");
+        int64_t n_opp = side == 0 ? nu : nm;
+        if (als_set_block(e, side, n_rows, row_off, n_opp, rp.data(), col.data(), rat.data()) != ALS_OK)
+            return die("set_block");
+        if (als_alloc_factors(e, side, n_slots) != ALS_OK) return die("alloc");
+    }
+    std::vector<float> U0((size_t)nu * k);
+    if (als_dataset_init_user_factors(ds, k, seed, 1, U0.data(), k, nu) != ALS_OK) return die("init");
+    if (precision == ALS_F32) {
+        if (als_write_factors(e, ALS_SIDE_USER, 0, nu, U0.data(), k) != ALS_OK) return die("upload");
+    } else {
+        std::vector<double> u64(U0.begin(), U0.end());
+        if (als_write_factors(e, ALS_SIDE_USER, 0, nu, u64.data(), k) != ALS_OK) return die("upload");
+    }
+    struct timeval t0, t1;
+    gettimeofday(&t0, nullptr);
+    for (long long it = 0; it < N; ++it) {
+        if (als_solve_half(e, ALS_SIDE_MOVIE, lambda) != ALS_OK) return die("solve movies");
+        if (als_solve_half(e, ALS_SIDE_USER, lambda) != ALS_OK) return die("solve users");
+    }
+    if (als_synchronize(e) != ALS_OK) return die("sync");
+    gettimeofday(&t1, nullptr);
+    const double secs = (t1.tv_sec - t0.tv_sec) + 1e-6 * (t1.tv_usec - t0.tv_usec);
+    double se = 0;
+    int64_t cnt = 0;
+    if (als_sq_error(e, ALS_SIDE_MOVIE, &se, &cnt) != ALS_OK) return die("sq_error");
+    printf("ALS: %lld iterations in %.3f s (%.3e ratings/s per iteration); MSE %.6f RMSE %.6f\n", N, secs,
+           N > 0 ? (double)nnz * N / secs : 0.0, cnt ? se / cnt : 0.0, cnt ? std::sqrt(se / cnt) : 0.0);
+
+    // FeatureCollector: factors in ascending id order (slot order for one shard).
+    printf("Start Prediction Matrix Computation at %s\n", java_timestamp().c_str());
+    std::vector<float> U((size_t)nu * k), M((size_t)nm * k);
+    if (precision == ALS_F32) {
+        if (als_read_factors(e, ALS_SIDE_USER, 0, nu, U.data(), k) != ALS_OK) return die("read");
+        if (als_read_factors(e, ALS_SIDE_MOVIE, 0, nm, M.data(), k) != ALS_OK) return die("read");
+    } else {
+        std::vector<double> u64((size_t)nu * k), m64((size_t)nm * k);
+        if (als_read_factors(e, ALS_SIDE_USER, 0, nu, u64.data(), k) != ALS_OK) return die("read");
+        if (als_read_factors(e, ALS_SIDE_MOVIE, 0, nm, m64.data(), k) != ALS_OK) return die("read");
+        for (size_t i = 0; i < U.size(); ++i) U[i] = (float)u64[i];
+        for (size_t i = 0; i < M.size(); ++i) M[i] = (float)m64[i];
+    }
+    mkdir(outdir.c_str(), 0755);
+    const std::string path = outdir + "/prediction_matrix_" + java_timestamp();
+    printf("Done at %s\n", java_timestamp().c_str());
+    if (als_write_prediction_csv(path.c_str(), U.data(), nu, k, M.data(), nm, k, k) != ALS_OK) return die("csv");
+    printf("Prediction matrix: %s\n", path.c_str());
+    als_engine_destroy(e);
+    als_dataset_destroy(ds);
+    return 0;
+}

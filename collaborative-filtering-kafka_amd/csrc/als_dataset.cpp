@@ -1,0 +1,591 @@
+// als_dataset.cpp -- host data layer (include/als_host.h): Netflix-format ingest, in-block (CSR) build,
+// id % G sharding into slot order, seeded U0, synthetic Netflix-shape generator, prediction CSV.
+#include <algorithm>
+#include <charconv>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <numeric>
+#include <random>
+#include <string>
+#include <vector>
+
+#include <atomic>
+#include <thread>
+
+#include "als_host.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+}  // namespace
+
+// als_last_error() is defined in als_engine.cpp; the data layer keeps its own thread-local message and
+// exposes it through the same accessor by forwarding on failure.
+extern "C" const char* als_last_error(void);
+namespace cfk_detail {
+void set_last_error(const std::string& s);
+}
+
+struct als_dataset {
+    // arrival order (the producer's send order, NetflixDataFormatProducer.java:58)
+    std::vector<int32_t> movie, user;
+    std::vector<int16_t> rating;
+    // derived
+    std::vector<int64_t> ids[2];      // ascending raw ids per side (0 = movie, 1 = user)
+    std::vector<int32_t> dense[2];    // per rating: dense (ascending-id rank) index of its movie / user
+};
+
+namespace {
+
+int report(int code) {
+    if (code != ALS_OK) cfk_detail::set_last_error(g_err);
+    return code;
+}
+
+void finalize(als_dataset* ds) {
+    const int64_t n = (int64_t)ds->rating.size();
+    for (int s = 0; s < 2; ++s) {
+        const std::vector<int32_t>& raw = s == 0 ? ds->movie : ds->user;
+        int32_t mx = 0;
+        for (int32_t v : raw) mx = std::max(mx, v);
+        // counting presence over [0, max] (ids are bounded by int32 and were checked >= 0)
+        std::vector<int32_t> rank((size_t)mx + 1, -1);
+        for (int32_t v : raw) rank[v] = 0;
+        ds->ids[s].clear();
+        for (int64_t v = 0; v <= mx; ++v)
+            if (rank[v] == 0) {
+                rank[v] = (int32_t)ds->ids[s].size();
+                ds->ids[s].push_back(v);
+            }
+        ds->dense[s].resize(n);
+        for (int64_t t = 0; t < n; ++t) ds->dense[s][t] = rank[raw[t]];
+    }
+}
+
+// Shard geometry of one side under G shards.
+struct ShardMap {
+    int G = 1;
+    int64_t S = 0;                        // slots per shard
+    std::vector<int64_t> slot;            // per dense entity
+    std::vector<int64_t> count;           // entities per shard
+};
+
+ShardMap shard_map(const als_dataset* ds, int side, int G) {
+    ShardMap m;
+    m.G = G;
+    const auto& ids = ds->ids[side];
+    m.count.assign(G, 0);
+    m.slot.resize(ids.size());
+    std::vector<int64_t> rank(ids.size());
+    for (size_t i = 0; i < ids.size(); ++i) {
+        const int sh = (int)(ids[i] % G);   // PureModStreamPartitioner.java:10
+        rank[i] = m.count[sh]++;
+    }
+    m.S = 0;
+    for (int64_t c : m.count) m.S = std::max(m.S, c);
+    for (size_t i = 0; i < ids.size(); ++i) m.slot[i] = (ids[i] % G) * m.S + rank[i];
+    return m;
+}
+
+// Java Double.toString layout over the shortest round-trip digits.
+std::string java_double(double v) {
+    if (std::isnan(v)) return "NaN";
+    if (std::isinf(v)) return v > 0 ? "Infinity" : "-Infinity";
+    if (v == 0.0) return std::signbit(v) ? "-0.0" : "0.0";
+    char buf[64];
+    auto res = std::to_chars(buf, buf + sizeof(buf), v, std::chars_format::scientific);
+    std::string s(buf, res.ptr);
+    std::string sign;
+    if (s[0] == '-') {
+        sign = "-";
+        s = s.substr(1);
+    }
+    const size_t epos = s.find('e');
+    const int exp10 = atoi(s.c_str() + epos + 1);
+    std::string digits;
+    for (size_t i = 0; i < epos; ++i)
+        if (s[i] != '.') digits.push_back(s[i]);
+    const double a = std::fabs(v);
+    std::string out;
+    if (a >= 1e-3 && a < 1e7) {
+        if (exp10 >= 0) {
+            std::string ip = digits.substr(0, std::min<size_t>(digits.size(), (size_t)exp10 + 1));
+            while ((int)ip.size() < exp10 + 1) ip.push_back('0');
+            std::string fp = digits.size() > (size_t)exp10 + 1 ? digits.substr(exp10 + 1) : "0";
+            out = ip + "." + fp;
+        } else {
+            out = "0." + std::string((size_t)(-exp10 - 1), '0') + digits;
+        }
+    } else {
+        out = digits.substr(0, 1) + "." + (digits.size() > 1 ? digits.substr(1) : "0") + "E" + std::to_string(exp10);
+    }
+    return sign + out;
+}
+
+uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+struct Rng {   // xoshiro256** seeded by splitmix64
+    uint64_t s[4];
+    explicit Rng(uint64_t seed) {
+        for (auto& w : s) w = seed = mix64(seed);
+    }
+    static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+    uint64_t next() {
+        const uint64_t r = rotl(s[1] * 5, 7) * 9, t = s[1] << 17;
+        s[2] ^= s[0];
+        s[3] ^= s[1];
+        s[1] ^= s[2];
+        s[0] ^= s[3];
+        s[2] ^= t;
+        s[3] = rotl(s[3], 45);
+        return r;
+    }
+    double uniform() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
+    uint64_t below(uint64_t n) { return (uint64_t)(((__uint128_t)next() * n) >> 64); }
+};
+
+}  // namespace
+
+extern "C" {
+
+float als_u01(uint64_t seed, int64_t raw_id, int32_t feature) {
+    const uint64_t h = mix64(seed ^ mix64((uint64_t)raw_id * 0x100000001B3ULL + (uint64_t)(uint32_t)feature));
+    return (float)(h >> 40) * (1.0f / 16777216.0f);
+}
+
+int als_dataset_load_netflix(const char* path, als_dataset** out) {
+    if (!path || !out) return report(fail(ALS_ERR_INVALID_ARGUMENT, "NULL argument"));
+    *out = nullptr;
+    FILE* f = fopen(path, "rb");
+    if (!f) return report(fail(ALS_ERR_IO, "cannot open %s", path));
+    std::unique_ptr<als_dataset> ds(new als_dataset());
+    std::vector<char> line(1 << 16);
+    int64_t current = -1;
+    int64_t lineno = 0;
+    auto parse_int = [](const char* b, const char* e, int64_t& v) -> bool {
+        // Integer.parseInt / Short.parseShort: optional sign, decimal digits only
+        if (b == e) return false;
+        bool neg = false;
+        if (*b == '-' || *b == '+') {
+            neg = *b == '-';
+            ++b;
+            if (b == e) return false;
+        }
+        int64_t x = 0;
+        for (; b < e; ++b) {
+            if (*b < '0' || *b > '9') return false;
+            x = x * 10 + (*b - '0');
+            if (x > (int64_t)1 << 40) return false;
+        }
+        v = neg ? -x : x;
+        return true;
+    };
+    while (fgets(line.data(), (int)line.size(), f)) {
+        ++lineno;
+        size_t n = strlen(line.data());
+        while (n > 0 && (line[n - 1] == '\n' || line[n - 1] == '\r')) --n;   // BufferedReader.readLine
+        const char* b = line.data();
+        const char* e = b + n;
+        if (n > 0 && b[n - 1] == ':') {                                   // row.endsWith(":")
+            const char* colon = (const char*)memchr(b, ':', n);           // row.split(":")[0]
+            int64_t v;
+            if (!parse_int(b, colon, v) || v < 0 || v > INT32_MAX) {
+                fclose(f);
+                return report(fail(ALS_ERR_PARSE, "%s:%lld: bad movie header", path, (long long)lineno));
+            }
+            current = v;
+            continue;
+        }
+        const char* c1 = (const char*)memchr(b, ',', n);
+        const char* c2 = c1 ? (const char*)memchr(c1 + 1, ',', e - c1 - 1) : nullptr;
+        const char* rend = c2 ? c2 : e;
+        int64_t uid, r;
+        if (!c1 || !parse_int(b, c1, uid) || !parse_int(c1 + 1, rend, r) || uid < 0 || uid > INT32_MAX ||
+            r < -32768 || r > 32767) {
+            fclose(f);
+            return report(fail(ALS_ERR_PARSE, "%s:%lld: expected UserID,Rating,Date", path, (long long)lineno));
+        }
+        if (current < 0) {
+            fclose(f);
+            return report(fail(ALS_ERR_PARSE, "%s:%lld: rating before the first movie header", path, (long long)lineno));
+        }
+        ds->movie.push_back((int32_t)current);
+        ds->user.push_back((int32_t)uid);
+        ds->rating.push_back((int16_t)r);
+    }
+    fclose(f);
+    finalize(ds.get());
+    *out = ds.release();
+    return ALS_OK;
+}
+
+int als_dataset_from_ratings(int64_t n, const int32_t* movie_ids, const int32_t* user_ids, const int16_t* ratings,
+                             als_dataset** out) {
+    if (!out || n < 0 || (n > 0 && (!movie_ids || !user_ids || !ratings)))
+        return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));
+    *out = nullptr;
+    for (int64_t t = 0; t < n; ++t)
+        if (movie_ids[t] < 0 || user_ids[t] < 0)
+            return report(fail(ALS_ERR_INVALID_ARGUMENT, "negative id at rating %lld", (long long)t));
+    std::unique_ptr<als_dataset> ds(new als_dataset());
+    ds->movie.assign(movie_ids, movie_ids + n);
+    ds->user.assign(user_ids, user_ids + n);
+    ds->rating.assign(ratings, ratings + n);
+    finalize(ds.get());
+    *out = ds.release();
+    return ALS_OK;
+}
+
+int als_dataset_synthetic_netflix(int64_t n_users, int64_t n_movies, int64_t nnz, uint64_t seed, int nthreads,
+                                  als_dataset** out) {
+    if (!out) return report(fail(ALS_ERR_INVALID_ARGUMENT, "out is NULL"));
+    *out = nullptr;
+    if (n_users < 1 || n_movies < 1 || n_users > INT32_MAX - 1 || n_movies > INT32_MAX - 1)
+        return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad entity counts"));
+    if (nnz < std::max(n_users, n_movies) || nnz > n_users * n_movies / 2)
+        return report(fail(ALS_ERR_INVALID_ARGUMENT, "nnz must be in [max(n_users, n_movies), n_users*n_movies/2]"));
+    if (nthreads <= 0) nthreads = (int)std::max(1u, std::thread::hardware_concurrency());
+    nthreads = std::min(nthreads, 64);
+    // --- user degrees: log-normal (median 96, mean 208.2 at Netflix scale), scaled to sum to nnz ---
+    const double mu = std::log(96.0), sigma = std::sqrt(2.0 * std::log(208.2 / 96.0));
+    const int64_t cap = std::min<int64_t>(17653, n_movies);
+    std::vector<int64_t> deg(n_users);
+    {
+        Rng rng(mix64(seed ^ 0xDE6DE6ULL));
+        std::vector<double> raw(n_users);
+        double sum = 0;
+        for (int64_t u = 0; u < n_users; ++u) {
+            // Box-Muller
+            double u1 = rng.uniform(), u2 = rng.uniform();
+            if (u1 < 1e-300) u1 = 1e-300;
+            const double z = std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2);
+            raw[u] = std::exp(mu + sigma * z);
+            sum += raw[u];
+        }
+        const double scale = (double)nnz / sum;
+        int64_t tot = 0;
+        for (int64_t u = 0; u < n_users; ++u) {
+            deg[u] = std::min<int64_t>(cap, std::max<int64_t>(1, (int64_t)std::llround(raw[u] * scale)));
+            tot += deg[u];
+        }
+        // exact total: adjust random users one rating at a time
+        while (tot != nnz) {
+            const int64_t u = (int64_t)rng.below(n_users);
+            if (tot < nnz && deg[u] < cap) { ++deg[u]; ++tot; }
+            else if (tot > nnz && deg[u] > 1) { --deg[u]; --tot; }
+        }
+    }
+    // --- movie popularity: w(rank) ~ (rank + 320)^-1.85 over a seeded random rank order ---
+    std::vector<double> w(n_movies);
+    std::vector<int32_t> perm(n_movies);
+    std::iota(perm.begin(), perm.end(), 0);
+    {
+        Rng rng(mix64(seed ^ 0x30F1EULL));
+        for (int64_t i = n_movies - 1; i > 0; --i) std::swap(perm[i], perm[rng.below(i + 1)]);
+        for (int64_t r = 0; r < n_movies; ++r) w[perm[r]] = std::pow((double)(r + 1) + 320.0, -1.85);
+    }
+    // alias table (Vose)
+    std::vector<double> prob(n_movies);
+    std::vector<int32_t> alias(n_movies);
+    {
+        const double tw = std::accumulate(w.begin(), w.end(), 0.0);
+        std::vector<double> p(n_movies);
+        std::vector<int32_t> small, large;
+        for (int64_t i = 0; i < n_movies; ++i) {
+            p[i] = w[i] * (double)n_movies / tw;
+            (p[i] < 1.0 ? small : large).push_back((int32_t)i);
+        }
+        while (!small.empty() && !large.empty()) {
+            const int32_t s = small.back(), l = large.back();
+            small.pop_back();
+            prob[s] = p[s];
+            alias[s] = l;
+            p[l] = (p[l] + p[s]) - 1.0;
+            if (p[l] < 1.0) {
+                large.pop_back();
+                small.push_back(l);
+            }
+        }
+        for (int32_t i : large) { prob[i] = 1.0; alias[i] = i; }
+        for (int32_t i : small) { prob[i] = 1.0; alias[i] = i; }
+    }
+    // rating histogram of data_sample_medium.txt: 1: 4.55%, 2: 9.78%, 3: 28.37%, 4: 33.51%, 5: 23.80%
+    const double cdf[5] = {0.0455, 0.0455 + 0.0978, 0.0455 + 0.0978 + 0.2837, 0.0455 + 0.0978 + 0.2837 + 0.3351, 1.0};
+    // --- per-user distinct movie lists (user-major), deterministic per user ---
+    std::vector<int64_t> uoff(n_users + 1, 0);
+    for (int64_t u = 0; u < n_users; ++u) uoff[u + 1] = uoff[u] + deg[u];
+    std::vector<int32_t> um(nnz);
+    std::vector<int16_t> ur(nnz);
+    {
+        std::atomic<int64_t> next_user{0};
+        auto worker = [&]() {
+            std::vector<int32_t> stamp(n_movies, -1);
+            for (;;) {
+                const int64_t u0 = next_user.fetch_add(256);
+                if (u0 >= n_users) break;
+                const int64_t u1 = std::min<int64_t>(n_users, u0 + 256);
+                for (int64_t u = u0; u < u1; ++u) {
+                    Rng rng(mix64(seed * 0x9E3779B97F4A7C15ULL + (uint64_t)u));
+                    const int64_t d = deg[u];
+                    int32_t* dst = um.data() + uoff[u];
+                    int64_t got = 0, tries = 0;
+                    const int64_t max_tries = 64 * d + 100000;
+                    while (got < d && tries < max_tries) {
+                        ++tries;
+                        const int64_t i = (int64_t)rng.below(n_movies);
+                        const int32_t m = rng.uniform() < prob[i] ? (int32_t)i : alias[i];
+                        if (stamp[m] == (int32_t)u) continue;
+                        stamp[m] = (int32_t)u;
+                        dst[got++] = m;
+                    }
+                    for (int64_t m = (int64_t)rng.below(n_movies); got < d; m = (m + 1) % n_movies)   // fallback
+                        if (stamp[m] != (int32_t)u) {
+                            stamp[m] = (int32_t)u;
+                            dst[got++] = (int32_t)m;
+                        }
+                    std::sort(dst, dst + d);
+                    for (int64_t t = 0; t < d; ++t) {
+                        const double x = rng.uniform();
+                        int r = 0;
+                        while (r < 4 && x >= cdf[r]) ++r;
+                        ur[uoff[u] + t] = (int16_t)(r + 1);
+                    }
+                }
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int i = 0; i < nthreads; ++i) pool.emplace_back(worker);
+        for (auto& t : pool) t.join();
+    }
+    // --- every movie rated at least once: re-point one entry of a popular movie (keeps nnz exact) ---
+    {
+        std::vector<int64_t> mdeg(n_movies, 0);
+        for (int64_t t = 0; t < nnz; ++t) ++mdeg[um[t]];
+        Rng rng(mix64(seed ^ 0xF111ULL));
+        for (int64_t m = 0; m < n_movies; ++m) {
+            if (mdeg[m] > 0) continue;
+            for (;;) {
+                const int64_t t = (int64_t)rng.below(nnz);
+                if (mdeg[um[t]] < 2) continue;
+                // owning user of entry t
+                const int64_t u = (int64_t)(std::upper_bound(uoff.begin(), uoff.end(), t) - uoff.begin()) - 1;
+                const int32_t* b = um.data() + uoff[u];
+                const int32_t* e = um.data() + uoff[u + 1];
+                if (std::binary_search(b, e, (int32_t)m)) continue;
+                --mdeg[um[t]];
+                um[t] = (int32_t)m;
+                ++mdeg[m];
+                std::sort(um.data() + uoff[u], um.data() + uoff[u + 1]);   // keep the row sorted (ratings stay iid)
+                break;
+            }
+        }
+    }
+    // --- movie-major arrival order (stable counting sort by movie; users ascending inside a movie) ---
+    std::unique_ptr<als_dataset> ds(new als_dataset());
+    {
+        std::vector<int64_t> moff(n_movies + 1, 0);
+        for (int64_t t = 0; t < nnz; ++t) ++moff[um[t] + 1];
+        for (int64_t m = 0; m < n_movies; ++m) moff[m + 1] += moff[m];
+        ds->movie.resize(nnz);
+        ds->user.resize(nnz);
+        ds->rating.resize(nnz);
+        std::vector<int64_t> pos(moff.begin(), moff.end() - 1);
+        for (int64_t u = 0; u < n_users; ++u)
+            for (int64_t t = uoff[u]; t < uoff[u + 1]; ++t) {
+                const int64_t p = pos[um[t]]++;
+                ds->movie[p] = um[t] + 1;
+                ds->user[p] = (int32_t)(u + 1);
+                ds->rating[p] = ur[t];
+            }
+        // dense ranks are known directly: ids are 1..n and every entity is rated
+        ds->ids[0].resize(n_movies);
+        ds->ids[1].resize(n_users);
+        std::iota(ds->ids[0].begin(), ds->ids[0].end(), 1);
+        std::iota(ds->ids[1].begin(), ds->ids[1].end(), 1);
+        ds->dense[0].resize(nnz);
+        ds->dense[1].resize(nnz);
+        for (int64_t t = 0; t < nnz; ++t) {
+            ds->dense[0][t] = ds->movie[t] - 1;
+            ds->dense[1][t] = ds->user[t] - 1;
+        }
+    }
+    *out = ds.release();
+    return ALS_OK;
+}
+
+int als_dataset_destroy(als_dataset* ds) {
+    delete ds;
+    return ALS_OK;
+}
+
+int als_dataset_counts(const als_dataset* ds, int64_t* n_movies, int64_t* n_users, int64_t* nnz) {
+    if (!ds) return report(fail(ALS_ERR_INVALID_ARGUMENT, "dataset is NULL"));
+    if (n_movies) *n_movies = (int64_t)ds->ids[0].size();
+    if (n_users) *n_users = (int64_t)ds->ids[1].size();
+    if (nnz) *nnz = (int64_t)ds->rating.size();
+    return ALS_OK;
+}
+
+int als_dataset_ids(const als_dataset* ds, int side, int64_t* ids) {
+    if (!ds || (side != 0 && side != 1) || !ids) return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));
+    std::copy(ds->ids[side].begin(), ds->ids[side].end(), ids);
+    return ALS_OK;
+}
+
+int als_dataset_ratings(const als_dataset* ds, int32_t* movie_ids, int32_t* user_ids, int16_t* ratings) {
+    if (!ds) return report(fail(ALS_ERR_INVALID_ARGUMENT, "dataset is NULL"));
+    if (movie_ids) std::copy(ds->movie.begin(), ds->movie.end(), movie_ids);
+    if (user_ids) std::copy(ds->user.begin(), ds->user.end(), user_ids);
+    if (ratings) std::copy(ds->rating.begin(), ds->rating.end(), ratings);
+    return ALS_OK;
+}
+
+int als_dataset_count_duplicates(const als_dataset* ds, int64_t* n_dup) {
+    if (!ds || !n_dup) return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));
+    const int64_t n = (int64_t)ds->rating.size();
+    std::vector<uint64_t> key(n);
+    for (int64_t t = 0; t < n; ++t) key[t] = ((uint64_t)(uint32_t)ds->dense[1][t] << 32) | (uint32_t)ds->dense[0][t];
+    std::sort(key.begin(), key.end());
+    int64_t d = 0;
+    for (int64_t t = 1; t < n; ++t) d += key[t] == key[t - 1];
+    *n_dup = d;
+    return ALS_OK;
+}
+
+int als_dataset_shard_info(const als_dataset* ds, int side, int n_shards, int shard, int64_t* n_rows,
+                           int64_t* row_offset, int64_t* nnz, int64_t* slots_per_shard, int64_t* n_slots) {
+    if (!ds || (side != 0 && side != 1) || n_shards < 1 || shard < 0 || shard >= n_shards)
+        return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));
+    const ShardMap m = shard_map(ds, side, n_shards);
+    int64_t z = 0;
+    const auto& raw = side == 0 ? ds->movie : ds->user;
+    for (int32_t v : raw) z += (v % n_shards) == shard;
+    if (n_rows) *n_rows = m.count[shard];
+    if (row_offset) *row_offset = shard * m.S;
+    if (nnz) *nnz = z;
+    if (slots_per_shard) *slots_per_shard = m.S;
+    if (n_slots) *n_slots = m.S * n_shards;
+    return ALS_OK;
+}
+
+int als_dataset_shard_block(const als_dataset* ds, int side, int n_shards, int64_t shard, int64_t* row_ptr,
+                            int32_t* col_idx, int16_t* ratings, int64_t* row_ids) {
+    if (!ds || (side != 0 && side != 1) || n_shards < 1 || shard < 0 || shard >= n_shards || !row_ptr)
+        return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));
+    const int opp = 1 - side;
+    const ShardMap ms = shard_map(ds, side, n_shards);
+    const ShardMap mo = shard_map(ds, opp, n_shards);
+    const int64_t nr = ms.count[shard];
+    const int64_t base = shard * ms.S;
+    const auto& dn = ds->dense[side];
+    const auto& dop = ds->dense[opp];
+    const int64_t n = (int64_t)dn.size();
+    // stable counting sort of arrival order by local row: in-block order = arrival order
+    std::fill(row_ptr, row_ptr + nr + 1, 0);
+    for (int64_t t = 0; t < n; ++t) {
+        const int64_t s = ms.slot[dn[t]];
+        if (s >= base && s < base + nr) ++row_ptr[s - base + 1];
+    }
+    for (int64_t i = 0; i < nr; ++i) row_ptr[i + 1] += row_ptr[i];
+    if (col_idx || ratings) {
+        std::vector<int64_t> pos(row_ptr, row_ptr + nr);
+        for (int64_t t = 0; t < n; ++t) {
+            const int64_t s = ms.slot[dn[t]];
+            if (s < base || s >= base + nr) continue;
+            const int64_t p = pos[s - base]++;
+            if (col_idx) col_idx[p] = (int32_t)mo.slot[dop[t]];
+            if (ratings) ratings[p] = ds->rating[t];
+        }
+    }
+    if (row_ids) {
+        const auto& ids = ds->ids[side];
+        for (size_t i = 0; i < ids.size(); ++i) {
+            const int64_t s = ms.slot[i];
+            if (s >= base && s < base + nr) row_ids[s - base] = ids[i];
+        }
+    }
+    return ALS_OK;
+}
+
+int als_dataset_slots(const als_dataset* ds, int side, int n_shards, int64_t* slot_of) {
+    if (!ds || (side != 0 && side != 1) || n_shards < 1 || !slot_of)
+        return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));
+    const ShardMap m = shard_map(ds, side, n_shards);
+    std::copy(m.slot.begin(), m.slot.end(), slot_of);
+    return ALS_OK;
+}
+
+int als_dataset_init_user_factors(const als_dataset* ds, int num_features, uint64_t seed, int n_shards, float* out,
+                                  int64_t ld, int64_t n_out_rows) {
+    if (!ds || num_features < 1 || n_shards < 1 || !out || ld < num_features)
+        return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));
+    const ShardMap m = shard_map(ds, 1, n_shards);
+    if (n_out_rows < m.S * n_shards) return report(fail(ALS_ERR_INVALID_ARGUMENT, "output has too few rows"));
+    std::fill(out, out + n_out_rows * ld, 0.f);
+    const int64_t nu = (int64_t)ds->ids[1].size();
+    std::vector<int64_t> sum(nu, 0), cnt(nu, 0);
+    for (size_t t = 0; t < ds->rating.size(); ++t) {
+        sum[ds->dense[1][t]] += ds->rating[t];
+        ++cnt[ds->dense[1][t]];
+    }
+    for (int64_t u = 0; u < nu; ++u) {
+        float* f = out + m.slot[u] * ld;
+        // DoubleStream.average() (exact for short ratings) cast to float; orElse(1.0)
+        const double mean = cnt[u] > 0 ? (double)sum[u] / (double)cnt[u] : 1.0;
+        f[0] = (float)mean;
+        for (int c = 1; c < num_features; ++c) f[c] = als_u01(seed, ds->ids[1][u], c);
+    }
+    return ALS_OK;
+}
+
+int als_write_prediction_csv(const char* path, const float* U, int64_t n_users, int64_t ldu, const float* M,
+                             int64_t n_movies, int64_t ldm, int num_features) {
+    if (!path || (n_users > 0 && !U) || (n_movies > 0 && !M) || num_features < 1 || ldu < num_features ||
+        ldm < num_features)
+        return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));
+    FILE* f = fopen(path, "wb");
+    if (!f) return report(fail(ALS_ERR_IO, "cannot create %s", path));
+    fprintf(f, "%lld %lld real\n", (long long)n_users, (long long)n_movies);
+    std::string line;
+    for (int64_t i = 0; i < n_users; ++i) {
+        line.clear();
+        const float* x = U + i * ldu;
+        for (int64_t j = 0; j < n_movies; ++j) {
+            const float* y = M + j * ldm;
+            float total = 0.f;   // MatrixMatrixMult_FDRM.multTransB: sequential fp32 dot
+            for (int c = 0; c < num_features; ++c) total += x[c] * y[c];
+            line += java_double((double)total);
+            line.push_back(' ');
+        }
+        line.push_back('\n');
+        if (fwrite(line.data(), 1, line.size(), f) != line.size()) {
+            fclose(f);
+            return report(fail(ALS_ERR_IO, "write failed: %s", path));
+        }
+    }
+    if (fclose(f) != 0) return report(fail(ALS_ERR_IO, "close failed: %s", path));
+    return ALS_OK;
+}
+
+}  // extern "C"

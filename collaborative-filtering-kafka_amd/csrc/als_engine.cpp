@@ -1,0 +1,531 @@
+// als_engine.cpp -- the C ABI of include/als.h: engine lifetime, in-block upload + work plan, factor
+// buffers, and the half-iteration launch. See include/als.h for the reference interface each entry
+// point replaces.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "als.h"
+#include "als_internal.h"
+
+using cfk::Path;
+using cfk::Task;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess)                                                                      \
+            return fail(ALS_ERR_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),     \
+                        __FILE__, __LINE__);                                                       \
+    } while (0)
+
+struct Block {
+    bool set = false;
+    int64_t n_rows = 0, row_offset = 0, n_opp_rows = 0, nnz = 0, nnz_padded = 0;
+    int32_t* d_col = nullptr;
+    float* d_rat = nullptr;
+    Task* d_tasks = nullptr;        // FULL + PARTIAL, sorted by work (longest first)
+    Task* d_reduce = nullptr;       // REDUCE
+    int32_t n_tasks = 0, n_reduce = 0, n_slots = 0;
+    double* d_task_se = nullptr;    // per-task squared-error partials
+};
+
+struct TimingRec {
+    int side;
+    hipEvent_t ev[3];
+};
+
+struct Factors {
+    void* ptr = nullptr;
+    int64_t n_rows = 0;
+    bool owned = false;
+};
+
+}  // namespace
+
+namespace cfk_detail {
+void set_last_error(const std::string& s) { g_last_error = s; }
+}  // namespace cfk_detail
+
+struct als_engine {
+    int device = 0;
+    int k = 0, kp = 0;
+    int precision = ALS_F32;
+    Path path = Path::VALU;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    Block blk[2];
+    Factors fac[2];
+    void* d_partials = nullptr;
+    size_t partial_bytes = 0;
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<TimingRec> pending;
+    size_t elem() const { return precision == ALS_F64 ? 8 : 4; }
+};
+
+namespace {
+
+int check_engine(const als_engine* e) {
+    if (!e) return fail(ALS_ERR_INVALID_ARGUMENT, "engine is NULL");
+    return ALS_OK;
+}
+int check_side(int side) {
+    if (side != ALS_SIDE_MOVIE && side != ALS_SIDE_USER)
+        return fail(ALS_ERR_INVALID_ARGUMENT, "side must be ALS_SIDE_MOVIE (0) or ALS_SIDE_USER (1), got %d", side);
+    return ALS_OK;
+}
+
+void free_block(Block& b) {
+    (void)hipFree(b.d_col);
+    (void)hipFree(b.d_rat);
+    (void)hipFree(b.d_tasks);
+    (void)hipFree(b.d_reduce);
+    (void)hipFree(b.d_task_se);
+    b = Block();
+}
+
+// Chunk length (entries, multiple of 4) above which a row is split into PARTIAL tasks + a REDUCE task.
+// Aim for enough wave-tasks to fill 256 CUs several times over while keeping partial traffic small.
+int64_t chunk_entries(int64_t nnz_padded) {
+    if (const char* env = getenv("ALS_CHUNK")) {
+        long v = atol(env);
+        if (v >= 4) return (v + 3) & ~3L;
+    }
+    int64_t c = nnz_padded / 24576;
+    c = std::max<int64_t>(c, 1024);
+    c = std::min<int64_t>(c, 8192);
+    return (c + 3) & ~int64_t(3);
+}
+
+}  // namespace
+
+extern "C" {
+
+int als_abi_version(void) { return ALS_ABI_VERSION; }
+const char* als_last_error(void) { return g_last_error.c_str(); }
+
+int als_engine_create(int device, int num_features, int precision, als_engine** out) {
+    if (!out) return fail(ALS_ERR_INVALID_ARGUMENT, "out is NULL");
+    *out = nullptr;
+    if (precision != ALS_F32 && precision != ALS_F64)
+        return fail(ALS_ERR_INVALID_ARGUMENT, "precision must be ALS_F32 or ALS_F64");
+    if (num_features < 1) return fail(ALS_ERR_INVALID_ARGUMENT, "num_features must be >= 1, got %d", num_features);
+    int kp = num_features <= 16 ? 16 : num_features <= 32 ? 32 : num_features <= 64 ? 64 : 128;
+    if (num_features > 64)
+        return fail(ALS_ERR_UNSUPPORTED, "num_features=%d: this build supports 1..64", num_features);
+    // MFMA Gram only where the accumulation is a real dense contraction (k >= 32, north star); fp64 and
+    // small k use the LDS-staged VALU Gram.
+    Path path = (precision == ALS_F32 && num_features >= 32) ? Path::MFMA : Path::VALU;
+    if (const char* env = getenv("ALS_FORCE_VALU"))
+        if (env[0] == '1') path = Path::VALU;
+    if (!cfk::variant_available(precision, kp, path))
+        return fail(ALS_ERR_UNSUPPORTED, "no kernel variant for precision=%d kp=%d", precision, kp);
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(ALS_ERR_INVALID_ARGUMENT, "device %d out of range (%d devices)", device, ndev);
+    HIP_TRY(hipSetDevice(device));
+    als_engine* e = new als_engine();
+    e->device = device;
+    e->k = num_features;
+    e->kp = kp;
+    e->precision = precision;
+    e->path = path;
+    hipError_t st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (st != hipSuccess) {
+        delete e;
+        return fail(ALS_ERR_DEVICE, "hipStreamCreate: %s", hipGetErrorString(st));
+    }
+    e->own_stream = true;
+    *out = e;
+    return ALS_OK;
+}
+
+int als_engine_destroy(als_engine* e) {
+    if (!e) return ALS_OK;
+    (void)hipSetDevice(e->device);
+    (void)hipStreamSynchronize(e->stream);
+    for (auto& b : e->blk) free_block(b);
+    for (auto& f : e->fac)
+        if (f.owned) (void)hipFree(f.ptr);
+    (void)hipFree(e->d_partials);
+    for (auto& rec : e->pending)
+        for (auto ev : rec.ev) (void)hipEventDestroy(ev);
+    for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
+    if (e->own_stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return ALS_OK;
+}
+
+int als_engine_set_stream(als_engine* e, void* hip_stream) {
+    if (int r = check_engine(e)) return r;
+    HIP_TRY(hipSetDevice(e->device));
+    if (e->own_stream) {
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        HIP_TRY(hipStreamDestroy(e->stream));
+        e->own_stream = false;
+        e->stream = nullptr;
+    }
+    if (hip_stream) {
+        e->stream = (hipStream_t)hip_stream;
+    } else {
+        HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+        e->own_stream = true;
+    }
+    return ALS_OK;
+}
+
+int als_factor_stride(const als_engine* e) { return e ? e->kp : 0; }
+
+int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows,
+                  const int64_t* row_ptr, const int32_t* col_idx, const int16_t* ratings) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    if (n_rows < 0 || row_offset < 0 || n_opp_rows < 0)
+        return fail(ALS_ERR_INVALID_ARGUMENT, "negative size (n_rows=%lld row_offset=%lld n_opp_rows=%lld)",
+                    (long long)n_rows, (long long)row_offset, (long long)n_opp_rows);
+    if (n_rows > INT32_MAX) return fail(ALS_ERR_UNSUPPORTED, "n_rows exceeds 2^31-1");
+    if (n_rows > 0 && !row_ptr) return fail(ALS_ERR_INVALID_ARGUMENT, "row_ptr is NULL");
+    const int64_t nnz = n_rows > 0 ? row_ptr[n_rows] : 0;
+    if (n_rows > 0 && row_ptr[0] != 0) return fail(ALS_ERR_INVALID_ARGUMENT, "row_ptr[0] must be 0");
+    if (nnz > 0 && (!col_idx || !ratings)) return fail(ALS_ERR_INVALID_ARGUMENT, "col_idx/ratings NULL");
+    // Validate the block on the host: a bad index would fault the GPU.
+    int64_t nnz_padded = 0;
+    for (int64_t i = 0; i < n_rows; ++i) {
+        const int64_t d = row_ptr[i + 1] - row_ptr[i];
+        if (d < 0) return fail(ALS_ERR_INVALID_ARGUMENT, "row_ptr not monotone at row %lld", (long long)i);
+        if (d > INT32_MAX / 2) return fail(ALS_ERR_UNSUPPORTED, "row %lld has %lld entries", (long long)i, (long long)d);
+        nnz_padded += (d + 3) & ~int64_t(3);
+    }
+    for (int64_t t = 0; t < nnz; ++t)
+        if (col_idx[t] < 0 || col_idx[t] >= n_opp_rows)
+            return fail(ALS_ERR_INVALID_ARGUMENT, "col_idx[%lld]=%d outside [0, %lld)", (long long)t, col_idx[t],
+                        (long long)n_opp_rows);
+
+    // Padded device in-block: every row starts on a multiple of 4 entries (one MFMA sub-step = 4
+    // entries); padding entries carry col = -1 and rating 0 and contribute nothing.
+    std::vector<int32_t> col(nnz_padded, -1);
+    std::vector<float> rat(nnz_padded, 0.f);
+    std::vector<int64_t> begin(n_rows + 1);
+    {
+        int64_t o = 0;
+        for (int64_t i = 0; i < n_rows; ++i) {
+            begin[i] = o;
+            const int64_t b = row_ptr[i], d = row_ptr[i + 1] - b;
+            for (int64_t t = 0; t < d; ++t) {
+                col[o + t] = col_idx[b + t];
+                rat[o + t] = (float)ratings[b + t];
+            }
+            o += (d + 3) & ~int64_t(3);
+        }
+        begin[n_rows] = o;
+    }
+    // Work plan.
+    const int64_t chunk = chunk_entries(nnz_padded);
+    std::vector<Task> tasks, reduce;
+    int64_t slots = 0;
+    for (int64_t i = 0; i < n_rows; ++i) {
+        const int64_t d = row_ptr[i + 1] - row_ptr[i];
+        const int64_t pl = (d + 3) & ~int64_t(3);
+        Task t{};
+        t.row = (int32_t)i;
+        t.ndeg = (int32_t)d;
+        if (pl <= chunk) {
+            t.begin = begin[i];
+            t.nsteps = (int32_t)(pl / 4);
+            t.slot = -1;
+            t.kind = cfk::TASK_FULL;
+            tasks.push_back(t);
+        } else {
+            const int64_t first = slots;
+            for (int64_t o = 0; o < pl; o += chunk) {
+                Task p = t;
+                p.begin = begin[i] + o;
+                p.nsteps = (int32_t)(std::min(chunk, pl - o) / 4);
+                p.slot = (int32_t)slots++;
+                p.kind = cfk::TASK_PARTIAL;
+                tasks.push_back(p);
+            }
+            Task r = t;
+            r.begin = 0;
+            r.slot = (int32_t)first;
+            r.nsteps = (int32_t)(slots - first);
+            r.kind = cfk::TASK_REDUCE;
+            reduce.push_back(r);
+        }
+    }
+    if (slots > INT32_MAX) return fail(ALS_ERR_UNSUPPORTED, "too many partial slots");
+    // Longest tasks first (LPT): the grid drains with a short tail.
+    std::stable_sort(tasks.begin(), tasks.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
+    std::stable_sort(reduce.begin(), reduce.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
+    if (tasks.size() > (size_t)INT32_MAX) return fail(ALS_ERR_UNSUPPORTED, "too many tasks");
+
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    Block& blk = e->blk[side];
+    free_block(blk);
+    blk.n_rows = n_rows;
+    blk.row_offset = row_offset;
+    blk.n_opp_rows = n_opp_rows;
+    blk.nnz = nnz;
+    blk.nnz_padded = nnz_padded;
+    blk.n_tasks = (int32_t)tasks.size();
+    blk.n_reduce = (int32_t)reduce.size();
+    blk.n_slots = (int32_t)slots;
+    auto up = [&](void** dst, const void* src, size_t bytes) -> int {
+        if (bytes == 0) return ALS_OK;
+        hipError_t st = hipMalloc(dst, bytes);
+        if (st != hipSuccess) return fail(ALS_ERR_OUT_OF_MEMORY, "hipMalloc(%zu): %s", bytes, hipGetErrorString(st));
+        st = hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice);
+        if (st != hipSuccess) return fail(ALS_ERR_DEVICE, "hipMemcpy: %s", hipGetErrorString(st));
+        return ALS_OK;
+    };
+    int r;
+    if ((r = up((void**)&blk.d_col, col.data(), col.size() * 4))) return r;
+    if ((r = up((void**)&blk.d_rat, rat.data(), rat.size() * 4))) return r;
+    if ((r = up((void**)&blk.d_tasks, tasks.data(), tasks.size() * sizeof(Task)))) return r;
+    if ((r = up((void**)&blk.d_reduce, reduce.data(), reduce.size() * sizeof(Task)))) return r;
+    if (!tasks.empty()) HIP_TRY(hipMalloc((void**)&blk.d_task_se, tasks.size() * sizeof(double)));
+    // Partial workspace sized for the larger side.
+    const size_t need = (size_t)slots * cfk::partial_words_per_lane(e->precision, e->kp, e->path) * 64 * e->elem();
+    if (need > e->partial_bytes) {
+        (void)hipFree(e->d_partials);
+        e->d_partials = nullptr;
+        e->partial_bytes = 0;
+        hipError_t st = hipMalloc(&e->d_partials, need);
+        if (st != hipSuccess) return fail(ALS_ERR_OUT_OF_MEMORY, "partials hipMalloc(%zu): %s", need, hipGetErrorString(st));
+        e->partial_bytes = need;
+    }
+    blk.set = true;
+    return ALS_OK;
+}
+
+int als_alloc_factors(als_engine* e, int side, int64_t n_total_rows) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    if (n_total_rows < 0) return fail(ALS_ERR_INVALID_ARGUMENT, "n_total_rows < 0");
+    HIP_TRY(hipSetDevice(e->device));
+    Factors& f = e->fac[side];
+    if (f.owned) (void)hipFree(f.ptr);
+    f = Factors();
+    const size_t bytes = (size_t)std::max<int64_t>(n_total_rows, 1) * e->kp * e->elem();
+    hipError_t st = hipMalloc(&f.ptr, bytes);
+    if (st != hipSuccess) return fail(ALS_ERR_OUT_OF_MEMORY, "factors hipMalloc(%zu): %s", bytes, hipGetErrorString(st));
+    f.owned = true;
+    f.n_rows = n_total_rows;
+    HIP_TRY(hipMemsetAsync(f.ptr, 0, bytes, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return ALS_OK;
+}
+
+int als_bind_factors(als_engine* e, int side, void* device_ptr, int64_t n_total_rows) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    if (!device_ptr || n_total_rows < 0) return fail(ALS_ERR_INVALID_ARGUMENT, "bad device buffer");
+    Factors& f = e->fac[side];
+    if (f.owned) (void)hipFree(f.ptr);
+    f.ptr = device_ptr;
+    f.n_rows = n_total_rows;
+    f.owned = false;
+    return ALS_OK;
+}
+
+int als_factors_device_ptr(const als_engine* e, int side, void** device_ptr, int64_t* n_total_rows) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    if (device_ptr) *device_ptr = e->fac[side].ptr;
+    if (n_total_rows) *n_total_rows = e->fac[side].n_rows;
+    return ALS_OK;
+}
+
+int als_write_factors(als_engine* e, int side, int64_t row0, int64_t n_rows, const void* host_src, int64_t src_ld) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    const Factors& f = e->fac[side];
+    if (!f.ptr) return fail(ALS_ERR_STATE, "factors of side %d not allocated/bound", side);
+    if (row0 < 0 || n_rows < 0 || row0 + n_rows > f.n_rows) return fail(ALS_ERR_INVALID_ARGUMENT, "row range out of bounds");
+    if (src_ld < e->k) return fail(ALS_ERR_INVALID_ARGUMENT, "src_ld (%lld) < num_features (%d)", (long long)src_ld, e->k);
+    if (n_rows == 0) return ALS_OK;
+    if (!host_src) return fail(ALS_ERR_INVALID_ARGUMENT, "host_src is NULL");
+    HIP_TRY(hipSetDevice(e->device));
+    const size_t es = e->elem();
+    // dst pitch = kp, width = k elements; the padding columns are zeroed first.
+    char* dst = (char*)f.ptr + (size_t)row0 * e->kp * es;
+    HIP_TRY(hipMemsetAsync(dst, 0, (size_t)n_rows * e->kp * es, e->stream));
+    HIP_TRY(hipMemcpy2DAsync(dst, e->kp * es, host_src, src_ld * es, e->k * es, n_rows, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return ALS_OK;
+}
+
+int als_read_factors(als_engine* e, int side, int64_t row0, int64_t n_rows, void* host_dst, int64_t dst_ld) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    const Factors& f = e->fac[side];
+    if (!f.ptr) return fail(ALS_ERR_STATE, "factors of side %d not allocated/bound", side);
+    if (row0 < 0 || n_rows < 0 || row0 + n_rows > f.n_rows) return fail(ALS_ERR_INVALID_ARGUMENT, "row range out of bounds");
+    if (dst_ld < e->k) return fail(ALS_ERR_INVALID_ARGUMENT, "dst_ld (%lld) < num_features (%d)", (long long)dst_ld, e->k);
+    if (n_rows == 0) return ALS_OK;
+    if (!host_dst) return fail(ALS_ERR_INVALID_ARGUMENT, "host_dst is NULL");
+    HIP_TRY(hipSetDevice(e->device));
+    const size_t es = e->elem();
+    const char* src = (const char*)f.ptr + (size_t)row0 * e->kp * es;
+    HIP_TRY(hipMemcpy2DAsync(host_dst, dst_ld * es, src, e->kp * es, e->k * es, n_rows, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return ALS_OK;
+}
+
+int als_solve_half(als_engine* e, int side, float lambda) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    Block& b = e->blk[side];
+    if (!b.set) return fail(ALS_ERR_STATE, "als_solve_half: no block set for side %d", side);
+    const Factors& self = e->fac[side];
+    const Factors& opp = e->fac[1 - side];
+    if (!self.ptr || !opp.ptr) return fail(ALS_ERR_STATE, "als_solve_half: factor matrices not allocated/bound");
+    if (b.row_offset + b.n_rows > self.n_rows)
+        return fail(ALS_ERR_STATE, "block rows [%lld,%lld) exceed factor rows %lld", (long long)b.row_offset,
+                    (long long)(b.row_offset + b.n_rows), (long long)self.n_rows);
+    if (b.n_opp_rows > opp.n_rows)
+        return fail(ALS_ERR_STATE, "block indexes %lld opposite rows, factor matrix has %lld", (long long)b.n_opp_rows,
+                    (long long)opp.n_rows);
+    if (!(lambda >= 0.f)) return fail(ALS_ERR_INVALID_ARGUMENT, "lambda must be >= 0");
+    HIP_TRY(hipSetDevice(e->device));
+    cfk::SolveArgs a{};
+    a.tasks = b.d_tasks;
+    a.n_tasks = b.n_tasks;
+    a.k = e->k;
+    a.col = b.d_col;
+    a.rat = b.d_rat;
+    a.opp = opp.ptr;
+    a.out = self.ptr;
+    a.row_offset = b.row_offset;
+    a.partials = e->d_partials;
+    a.lambda = lambda;
+    TimingRec rec{side, {nullptr, nullptr, nullptr}};
+    if (e->timing) {
+        for (auto& ev : rec.ev) {
+            if (!e->ev_pool.empty()) {
+                ev = e->ev_pool.back();
+                e->ev_pool.pop_back();
+            } else {
+                HIP_TRY(hipEventCreate(&ev));
+            }
+        }
+        HIP_TRY(hipEventRecord(rec.ev[0], e->stream));
+    }
+    HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream));
+    if (e->timing) HIP_TRY(hipEventRecord(rec.ev[1], e->stream));
+    if (b.n_reduce > 0) {
+        a.tasks = b.d_reduce;
+        a.n_tasks = b.n_reduce;
+        HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream));
+    }
+    if (e->timing) {
+        HIP_TRY(hipEventRecord(rec.ev[2], e->stream));
+        e->pending.push_back(rec);
+    }
+    return ALS_OK;
+}
+
+int als_sq_error(als_engine* e, int side, double* sum_sq_error, int64_t* count) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    Block& b = e->blk[side];
+    if (!b.set) return fail(ALS_ERR_STATE, "als_sq_error: no block set for side %d", side);
+    const Factors& self = e->fac[side];
+    const Factors& opp = e->fac[1 - side];
+    if (!self.ptr || !opp.ptr) return fail(ALS_ERR_STATE, "als_sq_error: factor matrices not allocated/bound");
+    HIP_TRY(hipSetDevice(e->device));
+    cfk::SqErrArgs a{};
+    a.tasks = b.d_tasks;
+    a.n_tasks = b.n_tasks;
+    a.col = b.d_col;
+    a.rat = b.d_rat;
+    a.opp = opp.ptr;
+    a.self = self.ptr;
+    a.row_offset = b.row_offset;
+    a.task_se = b.d_task_se;
+    HIP_TRY(cfk::launch_sq_error(e->precision, e->kp, a, e->stream));
+    std::vector<double> se(b.n_tasks);
+    if (b.n_tasks > 0)
+        HIP_TRY(hipMemcpyAsync(se.data(), b.d_task_se, se.size() * sizeof(double), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    double s = 0.0;
+    for (double v : se) s += v;   // fixed (task) order: deterministic
+    if (sum_sq_error) *sum_sq_error = s;
+    if (count) *count = b.nnz;
+    return ALS_OK;
+}
+
+int als_synchronize(als_engine* e) {
+    if (int r = check_engine(e)) return r;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return ALS_OK;
+}
+
+int als_set_timing(als_engine* e, int enabled) {
+    if (int r = check_engine(e)) return r;
+    e->timing = enabled != 0;
+    return ALS_OK;
+}
+
+int als_timing_collect(als_engine* e, int side, double* ms_gram, double* ms_reduce, int64_t* n_calls) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    HIP_TRY(hipSetDevice(e->device));
+    double g = 0, rd = 0;
+    int64_t n = 0;
+    std::vector<TimingRec> keep;
+    for (auto& rec : e->pending) {
+        if (rec.side != side) {
+            keep.push_back(rec);
+            continue;
+        }
+        HIP_TRY(hipEventSynchronize(rec.ev[2]));
+        float m1 = 0, m2 = 0;
+        HIP_TRY(hipEventElapsedTime(&m1, rec.ev[0], rec.ev[1]));
+        HIP_TRY(hipEventElapsedTime(&m2, rec.ev[1], rec.ev[2]));
+        g += m1;
+        rd += m2;
+        ++n;
+        for (auto ev : rec.ev) e->ev_pool.push_back(ev);
+    }
+    e->pending.swap(keep);
+    if (ms_gram) *ms_gram = g;
+    if (ms_reduce) *ms_reduce = rd;
+    if (n_calls) *n_calls = n;
+    return ALS_OK;
+}
+
+int als_block_stats(const als_engine* e, int side, int64_t* n_tasks, int64_t* n_reduce, int64_t* nnz_padded) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    const Block& b = e->blk[side];
+    if (n_tasks) *n_tasks = b.n_tasks;
+    if (n_reduce) *n_reduce = b.n_reduce;
+    if (nnz_padded) *nnz_padded = b.nnz_padded;
+    return ALS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,63 @@
+// Internal declarations shared by the engine (als_engine.cpp) and the kernels (als_kernels.hip).
+#pragma once
+#include <cstdint>
+
+#include <hip/hip_runtime.h>
+
+namespace cfk {
+
+// One wave-sized unit of work of a half-iteration (host-built once per uploaded block, README.md:146-147:
+// the rating blocks never change, so the work plan is fixed for every iteration).
+//   kind FULL    : gather rows [begin, begin + 4*nsteps) of the padded in-block, accumulate Gram + RHS,
+//                  regularise, Cholesky-solve, store factor row `row`.
+//   kind PARTIAL : same gather/accumulate over one chunk of a long row; store the raw per-lane
+//                  accumulators into partial slot `slot` (no solve).
+//   kind REDUCE  : sum partial slots [slot, slot + nsteps) of row `row` in fixed order, then solve + store.
+enum TaskKind : int32_t { TASK_FULL = 0, TASK_PARTIAL = 1, TASK_REDUCE = 2 };
+
+struct alignas(16) Task {
+    int64_t begin;   // entry offset into the padded col/rating arrays (multiple of 4)
+    int32_t nsteps;  // FULL/PARTIAL: number of 4-entry sub-steps; REDUCE: number of partial slots
+    int32_t row;     // local row of the block (factor row = row_offset + row)
+    int32_t slot;    // PARTIAL: slot written; REDUCE: first slot read; FULL: -1
+    int32_t ndeg;    // true in-block size n_j (lambda * n_j * I, MFeatureCalculator.java:92-95)
+    int32_t kind;
+    int32_t pad;
+};
+static_assert(sizeof(Task) == 32, "Task layout");
+
+struct SolveArgs {
+    const Task* tasks;
+    int32_t n_tasks;
+    int32_t k;              // true number of features (<= KP)
+    const int32_t* col;     // padded in-block opposite indices (-1 = padding)
+    const float* rat;       // padded ratings (0 = padding)
+    const void* opp;        // opposite factor matrix [n_opp][KP]
+    void* out;              // this side's factor matrix [n_total][KP]
+    int64_t row_offset;     // first factor row of this block
+    void* partials;         // partial-slot workspace
+    float lambda;
+};
+
+struct SqErrArgs {
+    const Task* tasks;      // FULL + PARTIAL tasks (they cover every entry exactly once)
+    int32_t n_tasks;
+    const int32_t* col;
+    const float* rat;
+    const void* opp;
+    const void* self;
+    int64_t row_offset;
+    double* task_se;        // [n_tasks]
+};
+
+enum class Path : int { VALU = 0, MFMA = 1 };
+
+// Launch helpers (defined in als_kernels.hip). Return hipSuccess or the launch error.
+hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s);
+hipError_t launch_sq_error(int precision, int kp, const SqErrArgs& a, hipStream_t s);
+// Per-lane accumulator words (elements of the engine precision) of one partial slot: nacc * 64.
+int partial_words_per_lane(int precision, int kp, Path path);
+// Host-side check that a (precision, kp, path) variant is compiled in.
+bool variant_available(int precision, int kp, Path path);
+
+}  // namespace cfk

@@ -1,0 +1,248 @@
+"""Python mirror of the reference's hot-path surface, over the C ABI of libcfk_als.so.
+
+Reference interface (paths under src/main/java/de/hpi/collaborativefilteringkafka/):
+  - ``Dataset``           ingest + in-block build + partition key: producers/NetflixDataFormatProducer.java:44-60,
+                          processors/MRatings2BlocksProcessor.java:48-69, processors/URatings2BlocksProcessor.java:72-92,
+                          producers/PureModStreamPartitioner.java:9-10 (all computed natively in als_dataset.cpp)
+  - ``ALSEngine``         one partition's MFeatureCalculator / UFeatureCalculator solve state
+                          (processors/MFeatureCalculator.java:49-136, processors/UFeatureCalculator.java:49-136)
+
+Device memory is torch-owned (factor matrices are torch tensors bound into the engine) so that
+``torch.distributed`` (RCCL over xGMI) can all-gather straight into the matrices the kernels read.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import F32, F64, SIDE_MOVIE, SIDE_USER, call, ptr
+
+SIDES = {"movie": SIDE_MOVIE, "user": SIDE_USER}
+
+
+def _side(s) -> int:
+    return SIDES[s] if isinstance(s, str) else int(s)
+
+
+def factor_stride(k: int) -> int:
+    return 16 if k <= 16 else 32 if k <= 32 else 64 if k <= 64 else 128
+
+
+class Dataset:
+    """Ratings in arrival order plus the derived in-blocks (native; see include/als_host.h)."""
+
+    def __init__(self, handle):
+        self._h = ctypes.c_void_p(handle)
+
+    # -- constructors ---------------------------------------------------------------------------
+    @classmethod
+    def load_netflix(cls, path: str) -> "Dataset":
+        h = ctypes.c_void_p()
+        call("als_dataset_load_netflix", path.encode(), ctypes.byref(h))
+        return cls(h.value)
+
+    @classmethod
+    def from_ratings(cls, movie_ids, user_ids, ratings) -> "Dataset":
+        m = np.ascontiguousarray(movie_ids, np.int32)
+        u = np.ascontiguousarray(user_ids, np.int32)
+        r = np.ascontiguousarray(ratings, np.int16)
+        h = ctypes.c_void_p()
+        call("als_dataset_from_ratings", len(m), ptr(m, ctypes.c_int32), ptr(u, ctypes.c_int32),
+             ptr(r, ctypes.c_int16), ctypes.byref(h))
+        return cls(h.value)
+
+    @classmethod
+    def synthetic_netflix(cls, n_users=480_189, n_movies=17_770, nnz=100_000_000, seed=0xA15, nthreads=0) -> "Dataset":
+        h = ctypes.c_void_p()
+        call("als_dataset_synthetic_netflix", n_users, n_movies, nnz, seed, nthreads, ctypes.byref(h))
+        return cls(h.value)
+
+    def close(self):
+        if self._h and self._h.value:
+            _lib.lib().als_dataset_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- queries ----------------------------------------------------------------------------------
+    def counts(self):
+        nm, nu, nnz = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        call("als_dataset_counts", self._h, ctypes.byref(nm), ctypes.byref(nu), ctypes.byref(nnz))
+        return nm.value, nu.value, nnz.value
+
+    @property
+    def n_movies(self):
+        return self.counts()[0]
+
+    @property
+    def n_users(self):
+        return self.counts()[1]
+
+    @property
+    def nnz(self):
+        return self.counts()[2]
+
+    def ids(self, side) -> np.ndarray:
+        side = _side(side)
+        n = self.counts()[0 if side == SIDE_MOVIE else 1]
+        out = np.zeros(n, np.int64)
+        call("als_dataset_ids", self._h, side, ptr(out, ctypes.c_int64))
+        return out
+
+    def ratings(self):
+        n = self.nnz
+        m = np.zeros(n, np.int32)
+        u = np.zeros(n, np.int32)
+        r = np.zeros(n, np.int16)
+        call("als_dataset_ratings", self._h, ptr(m, ctypes.c_int32), ptr(u, ctypes.c_int32), ptr(r, ctypes.c_int16))
+        return m, u, r
+
+    def count_duplicates(self) -> int:
+        d = ctypes.c_int64()
+        call("als_dataset_count_duplicates", self._h, ctypes.byref(d))
+        return d.value
+
+    def shard_info(self, side, n_shards=1, shard=0) -> dict:
+        v = [ctypes.c_int64() for _ in range(5)]
+        call("als_dataset_shard_info", self._h, _side(side), n_shards, shard, *[ctypes.byref(x) for x in v])
+        keys = ("n_rows", "row_offset", "nnz", "slots_per_shard", "n_slots")
+        return dict(zip(keys, (x.value for x in v)))
+
+    def shard_block(self, side, n_shards=1, shard=0) -> dict:
+        """In-block CSR of one shard: rows in ascending id, entries in arrival order, cols = opposite slots."""
+        info = self.shard_info(side, n_shards, shard)
+        rp = np.zeros(info["n_rows"] + 1, np.int64)
+        col = np.zeros(info["nnz"], np.int32)
+        rat = np.zeros(info["nnz"], np.int16)
+        ids = np.zeros(info["n_rows"], np.int64)
+        call("als_dataset_shard_block", self._h, _side(side), n_shards, shard, ptr(rp, ctypes.c_int64),
+             ptr(col, ctypes.c_int32), ptr(rat, ctypes.c_int16), ptr(ids, ctypes.c_int64))
+        info.update(row_ptr=rp, col=col, ratings=rat, row_ids=ids)
+        return info
+
+    def slots(self, side, n_shards=1) -> np.ndarray:
+        side = _side(side)
+        n = self.counts()[0 if side == SIDE_MOVIE else 1]
+        out = np.zeros(n, np.int64)
+        call("als_dataset_slots", self._h, side, n_shards, ptr(out, ctypes.c_int64))
+        return out
+
+    def init_user_factors(self, k: int, seed: int = 42, n_shards: int = 1, ld: int | None = None) -> np.ndarray:
+        """U0 in slot order (UFeatureInitializer.java:50-56 with the shared seeded generator)."""
+        ld = k if ld is None else ld
+        n_slots = self.shard_info(SIDE_USER, n_shards, 0)["n_slots"]
+        out = np.zeros((n_slots, ld), np.float32)
+        call("als_dataset_init_user_factors", self._h, k, seed, n_shards, ptr(out, ctypes.c_float), ld, n_slots)
+        return out
+
+
+def u01(seed: int, raw_id: int, feature: int) -> float:
+    return _lib.lib().als_u01(seed, raw_id, feature)
+
+
+def write_prediction_csv(path: str, U: np.ndarray, M: np.ndarray) -> None:
+    """FeatureCollector.calculatePredictionMatrix + saveDenseCSV (FeatureCollector.java:90-110)."""
+    U = np.ascontiguousarray(U, np.float32)
+    M = np.ascontiguousarray(M, np.float32)
+    k = U.shape[1]
+    call("als_write_prediction_csv", path.encode(), ptr(U, ctypes.c_float), U.shape[0], k, ptr(M, ctypes.c_float),
+         M.shape[0], k, k)
+
+
+class ALSEngine:
+    """One device engine: the in-blocks of this rank's shard of both sides + bound factor matrices."""
+
+    def __init__(self, k: int, precision: str = "f32", device: int = 0):
+        if precision not in ("f32", "f64"):
+            raise ValueError("precision must be 'f32' or 'f64'")
+        self.k = k
+        self.precision = precision
+        self.device = device
+        self.dtype = torch.float32 if precision == "f32" else torch.float64
+        self.np_dtype = np.float32 if precision == "f32" else np.float64
+        h = ctypes.c_void_p()
+        call("als_engine_create", device, k, F32 if precision == "f32" else F64, ctypes.byref(h))
+        self._h = h
+        self.kp = _lib.lib().als_factor_stride(self._h)
+        self.factors = [None, None]    # torch tensors [n_slots, kp]
+
+    def close(self):
+        if self._h and self._h.value:
+            _lib.lib().als_engine_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def use_torch_stream(self, stream: torch.cuda.Stream | None = None):
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        call("als_engine_set_stream", self._h, ctypes.c_void_p(s.cuda_stream))
+
+    def set_block(self, side, row_ptr, col, ratings, row_offset: int, n_opp_rows: int):
+        rp = np.ascontiguousarray(row_ptr, np.int64)
+        c = np.ascontiguousarray(col, np.int32)
+        r = np.ascontiguousarray(ratings, np.int16)
+        call("als_set_block", self._h, _side(side), len(rp) - 1, row_offset, n_opp_rows, ptr(rp, ctypes.c_int64),
+             ptr(c, ctypes.c_int32), ptr(r, ctypes.c_int16))
+
+    def bind_factors(self, side, tensor: torch.Tensor):
+        side = _side(side)
+        if tensor.dtype != self.dtype or tensor.dim() != 2 or tensor.shape[1] != self.kp or not tensor.is_contiguous():
+            raise ValueError(f"factor tensor must be contiguous [n, {self.kp}] {self.dtype}")
+        if tensor.device.type != "cuda":
+            raise ValueError("factor tensor must live on the GPU")
+        call("als_bind_factors", self._h, side, ctypes.c_void_p(tensor.data_ptr()), tensor.shape[0])
+        self.factors[side] = tensor
+
+    def alloc_factors(self, side, n_rows: int) -> torch.Tensor:
+        t = torch.zeros((max(n_rows, 1), self.kp), dtype=self.dtype, device=f"cuda:{self.device}")
+        self.bind_factors(side, t)
+        return t
+
+    def write_factors(self, side, host: np.ndarray, row0: int = 0):
+        h = np.ascontiguousarray(host, self.np_dtype)
+        call("als_write_factors", self._h, _side(side), row0, h.shape[0], h.ctypes.data_as(ctypes.c_void_p), h.shape[1])
+
+    def read_factors(self, side, row0: int = 0, n_rows: int | None = None) -> np.ndarray:
+        side = _side(side)
+        if n_rows is None:
+            n_rows = self.factors[side].shape[0] - row0
+        out = np.zeros((n_rows, self.k), self.np_dtype)
+        call("als_read_factors", self._h, side, row0, n_rows, out.ctypes.data_as(ctypes.c_void_p), self.k)
+        return out
+
+    def solve_half(self, side, lam: float):
+        """MFeatureCalculator (side='movie') / UFeatureCalculator (side='user') for every row of the block."""
+        call("als_solve_half", self._h, _side(side), float(np.float32(lam)))
+
+    def sq_error(self, side="movie"):
+        se = ctypes.c_double()
+        cnt = ctypes.c_int64()
+        call("als_sq_error", self._h, _side(side), ctypes.byref(se), ctypes.byref(cnt))
+        return se.value, cnt.value
+
+    def synchronize(self):
+        call("als_synchronize", self._h)
+
+    def set_timing(self, on: bool):
+        call("als_set_timing", self._h, 1 if on else 0)
+
+    def timing_collect(self, side):
+        g, r, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+        call("als_timing_collect", self._h, _side(side), ctypes.byref(g), ctypes.byref(r), ctypes.byref(n))
+        return g.value, r.value, n.value
+
+    def block_stats(self, side):
+        a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        call("als_block_stats", self._h, _side(side), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return {"n_tasks": a.value, "n_reduce": b.value, "nnz_padded": c.value}

@@ -1,0 +1,110 @@
+/*
+ * als.h -- C ABI of the MI355X-native ALS engine (libcfk_als.so).
+ *
+ * Drop-in boundary for the reference's one hot path: the per-movie / per-user regularised least-squares
+ * feature update that the Kafka Streams processors run
+ *     MFeatureCalculator.process   src/main/java/de/hpi/collaborativefilteringkafka/processors/MFeatureCalculator.java:49-136
+ *     UFeatureCalculator.process   .../processors/UFeatureCalculator.java:49-136
+ * whose arithmetic sits behind EJML CommonOps_FDRM (multTransA / scale / identity / add / invert / mult,
+ * MFeatureCalculator.java:85-99). A re-plumbed processor buffers its partition's half-iteration (the EOF
+ * barrier, UFeatureInitializer.java:37-41) and makes ONE als_solve_half() call instead of one EJML solve per
+ * entity. The JNI / Panama binding a maintainer adds on the Java side is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain C types only; every function returns an als_status (0 = ALS_OK) and never throws or longjmps
+ *    across the ABI. als_last_error() returns the calling thread's last message. (The reference ignores
+ *    EJML invert's boolean, MFeatureCalculator.java:98; this ABI reports failures instead.)
+ *  - One engine = one (device, num_features, precision). Engines are independent; one engine must not be
+ *    used from two threads at once (the reference runs each task's process() single-threaded,
+ *    BaseKafkaApp.java:51, so one engine per stream task / GPU is the intended use).
+ *  - "side" selects the entity type whose rows are recomputed: ALS_SIDE_MOVIE rows are solved from user
+ *    factors (MFeatureCalculator), ALS_SIDE_USER rows from movie factors (UFeatureCalculator).
+ *  - Factor matrices live in device memory with a padded row stride (als_factor_stride(): 16, 32, 64 or
+ *    128 elements); columns >= num_features are kept at zero by the engine.
+ */
+#ifndef CFK_ALS_H
+#define CFK_ALS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ALS_ABI_VERSION 1
+
+typedef enum {
+    ALS_OK = 0,
+    ALS_ERR_INVALID_ARGUMENT = 1,
+    ALS_ERR_UNSUPPORTED = 2,
+    ALS_ERR_DEVICE = 3,        /* HIP runtime error */
+    ALS_ERR_OUT_OF_MEMORY = 4,
+    ALS_ERR_STATE = 5,         /* call order violated (e.g. solve before a block was set) */
+    ALS_ERR_IO = 6,
+    ALS_ERR_PARSE = 7,
+    ALS_ERR_DATA = 8           /* input that hangs the reference (duplicate pair, count mismatch) */
+} als_status;
+
+typedef enum { ALS_SIDE_MOVIE = 0, ALS_SIDE_USER = 1 } als_side;
+typedef enum { ALS_F32 = 0, ALS_F64 = 1 } als_precision;
+
+typedef struct als_engine als_engine;
+
+/* ---- version / errors --------------------------------------------------------------------------- */
+int         als_abi_version(void);
+const char* als_last_error(void);
+
+/* ---- engine lifetime ---------------------------------------------------------------------------- */
+/* Replaces the per-task processor state of MFeatureCalculator/UFeatureCalculator.init (:29-46).
+ * num_features = ALSApp.NUM_FEATURES (ALSApp.java:18), 1..128 (f64: 1..64). */
+int als_engine_create(int device, int num_features, int precision, als_engine** out);
+int als_engine_destroy(als_engine* e);
+/* Launch on a caller-provided hipStream_t (e.g. torch's current stream); NULL = engine-owned stream. */
+int als_engine_set_stream(als_engine* e, void* hip_stream);
+int als_factor_stride(const als_engine* e);
+
+/* ---- in-block upload (constant over all iterations, README.md:146-147) ---------------------------- */
+/* Replaces the state stores m-inblocks-uid / m-inblocks-ratings (resp. u-*) that
+ * MRatings2BlocksProcessor.java:48-69 / URatings2BlocksProcessor.java:72-92 fill: one CSR row per entity
+ * of this partition, entries in in-block order. Row i is solved into factor row (row_offset + i) of
+ * `side`; col_idx[] are rows of the opposite side's factor matrix (0 <= col < n_opp_rows).
+ * Host pointers; copied to the device once. */
+int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows,
+                  const int64_t* row_ptr, const int32_t* col_idx, const int16_t* ratings);
+
+/* ---- factor matrices (device resident) ---------------------------------------------------------- */
+/* Engine-owned buffer of n_total_rows x stride elements (zeroed). */
+int als_alloc_factors(als_engine* e, int side, int64_t n_total_rows);
+/* Caller-owned device buffer (e.g. a torch tensor), row stride = als_factor_stride(e), padding columns
+ * must be zero. Lets a collective (RCCL all-gather) write straight into the matrix the engine reads. */
+int als_bind_factors(als_engine* e, int side, void* device_ptr, int64_t n_total_rows);
+int als_factors_device_ptr(const als_engine* e, int side, void** device_ptr, int64_t* n_total_rows);
+/* Host <-> device copies of rows [row0, row0+n_rows) with a host row stride of src_ld/dst_ld elements
+ * (>= num_features); element type = float (ALS_F32) or double (ALS_F64). */
+int als_write_factors(als_engine* e, int side, int64_t row0, int64_t n_rows, const void* host_src, int64_t src_ld);
+int als_read_factors(als_engine* e, int side, int64_t row0, int64_t n_rows, void* host_dst, int64_t dst_ld);
+
+/* ---- THE HOT PATH ------------------------------------------------------------------------------- */
+/* For every row j of `side`'s block: gather Y_S = opposite factor rows of its in-block, form
+ * A = Y_S^T Y_S + lambda * n_j * I and V = Y_S^T r, solve A m_j = V (Cholesky; A is SPD because
+ * lambda * n_j > 0) and store m_j. == MFeatureCalculator.java:66-104 / UFeatureCalculator.java:66-104
+ * for the whole partition. Asynchronous on the engine's stream. */
+int als_solve_half(als_engine* e, int side, float lambda);
+
+/* Sum of (r - x_row . y_col)^2 over the block's observed ratings and their count (the RMSE/MSE
+ * reduction of scripts/calculate_mse.py:78-90 computed on the device from the factors). Synchronous. */
+int als_sq_error(als_engine* e, int side, double* sum_sq_error, int64_t* count);
+
+int als_synchronize(als_engine* e);
+/* Device-time accounting with HIP events on the engine's stream (non-blocking while enabled): every
+ * als_solve_half records its gram/solve launch and its reduce launch; als_timing_collect waits for the
+ * recorded events of `side`, returns their summed milliseconds and call count, and clears them. */
+int als_set_timing(als_engine* e, int enabled);
+int als_timing_collect(als_engine* e, int side, double* ms_gram, double* ms_reduce, int64_t* n_calls);
+/* Work-plan statistics of the uploaded block (tasks, partial slots, padded nnz). */
+int als_block_stats(const als_engine* e, int side, int64_t* n_tasks, int64_t* n_reduce, int64_t* nnz_padded);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFK_ALS_H */

@@ -1,0 +1,83 @@
+/*
+ * als_host.h -- host-side data layer of libcfk_als.so (C ABI).
+ *
+ * These are the callers on either side of the hot path, restated natively:
+ *   - ingest:   NetflixDataFormatProducer.runProducer      producers/NetflixDataFormatProducer.java:44-60
+ *   - blocks:   MRatings2BlocksProcessor / URatings2BlocksProcessor (in-blocks = CSR rows in arrival order)
+ *               processors/MRatings2BlocksProcessor.java:48-69, processors/URatings2BlocksProcessor.java:72-92
+ *   - sharding: PureModStreamPartitioner.partition = key % numPartitions   producers/PureModStreamPartitioner.java:9-10
+ *   - U0:       UFeatureInitializer.process (f[0] = mean rating, f[1..] uniform [0,1))   processors/UFeatureInitializer.java:43-56
+ *   - output:   FeatureCollector.calculatePredictionMatrix + EJML MatrixIO.saveDenseCSV   processors/FeatureCollector.java:72-110
+ * plus the seeded synthetic Netflix-shape generator used by the benchmark (BASELINE.json configs[2]).
+ *
+ * Slot layout for G shards (G = 1 for one GPU): entities of a side are sharded by raw_id % G; inside a
+ * shard they are ordered by ascending raw id; slot = shard * S + rank_in_shard with S = the largest shard
+ * size. The factor matrix of a side has G * S rows in slot order, so an all-gather of equal S-row shards
+ * IS the full matrix. For G = 1, slot = rank of the raw id among all ids of that side (= the collector's
+ * TreeMap order, FeatureCollector.java:21-22).
+ */
+#ifndef CFK_ALS_HOST_H
+#define CFK_ALS_HOST_H
+
+#include <stdint.h>
+
+#include "als.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct als_dataset als_dataset;
+
+/* Netflix format: "MovieID:" header lines, then "UserID,Rating,Date" lines (date ignored). Lines are
+ * parsed exactly as NetflixDataFormatProducer.java:44-60; a malformed line is ALS_ERR_PARSE (the reference
+ * producer throws NumberFormatException). Ids must be >= 0 (partition = id % P). */
+int als_dataset_load_netflix(const char* path, als_dataset** out);
+/* Ratings given in arrival order (movie id, user id, rating) -- e.g. records of movieIds-with-ratings. */
+int als_dataset_from_ratings(int64_t n, const int32_t* movie_ids, const int32_t* user_ids, const int16_t* ratings,
+                             als_dataset** out);
+/* Synthetic Netflix-shape data: user degrees log-normal (median 96, mean ~208, cap 17,653),
+ * movie popularity ~ (rank + 320)^-1.85 over a seeded random rank order, ratings drawn from the medium
+ * sample's histogram, no duplicate (user, movie) pairs, every entity rated at least once, exactly nnz
+ * ratings. Ids are 1..n. Arrival order is movie-major (like the Netflix files). nthreads <= 0: all cores. */
+int als_dataset_synthetic_netflix(int64_t n_users, int64_t n_movies, int64_t nnz, uint64_t seed, int nthreads,
+                                  als_dataset** out);
+int als_dataset_destroy(als_dataset* ds);
+
+int als_dataset_counts(const als_dataset* ds, int64_t* n_movies, int64_t* n_users, int64_t* nnz);
+/* Raw ids of a side in ascending order (n_movies or n_users entries). */
+int als_dataset_ids(const als_dataset* ds, int side, int64_t* ids);
+/* Arrival-order triples (any pointer may be NULL). */
+int als_dataset_ratings(const als_dataset* ds, int32_t* movie_ids, int32_t* user_ids, int16_t* ratings);
+/* Number of repeated (user, movie) pairs: the reference's readiness check (MFeatureCalculator.java:65)
+ * never fires for such an entity, so the reference hangs; callers reject them (ALS_ERR_DATA). */
+int als_dataset_count_duplicates(const als_dataset* ds, int64_t* n_dup);
+
+/* Shard `shard` of `side` under G = n_shards: rows, the shard's first slot, its entry count, slots per
+ * shard (S) and total slots (G * S) of this side. */
+int als_dataset_shard_info(const als_dataset* ds, int side, int n_shards, int shard, int64_t* n_rows,
+                           int64_t* row_offset, int64_t* nnz, int64_t* slots_per_shard, int64_t* n_slots);
+/* The shard's in-block CSR: row_ptr[n_rows+1], col_idx[nnz] = opposite-side SLOTS under the same G,
+ * ratings[nnz], row_ids[n_rows] = raw ids (any of col/ratings/row_ids may be NULL). */
+int als_dataset_shard_block(const als_dataset* ds, int side, int n_shards, int64_t shard, int64_t* row_ptr,
+                            int32_t* col_idx, int16_t* ratings, int64_t* row_ids);
+/* slot_of[i] = slot of the i-th entity of `side` in ascending raw-id order. */
+int als_dataset_slots(const als_dataset* ds, int side, int n_shards, int64_t* slot_of);
+/* U0 for every user, written at its slot row (out has n_out_rows >= n_slots rows of ld >= k floats;
+ * unused slot rows are zeroed). f[0] = (float)mean(ratings) in double (UFeatureInitializer.java:50),
+ * f[1..k-1] = u01(seed, raw user id, f): the reference's unseeded Math.random() (UFeatureInitializer.java:55)
+ * replaced by a shared counter-based generator (splitmix64; exact floats in [0,1)). */
+int als_dataset_init_user_factors(const als_dataset* ds, int num_features, uint64_t seed, int n_shards,
+                                  float* out, int64_t ld, int64_t n_out_rows);
+float als_u01(uint64_t seed, int64_t raw_id, int32_t feature);
+
+/* FeatureCollector.calculatePredictionMatrix (:90-110): P = U M^T in fp32 (rows: users ascending, columns:
+ * movies ascending), widened to double, written in EJML saveDenseCSV layout ("R C real" header, every value
+ * followed by one space, one row per line) with Java Double.toString-style shortest round-trip values. */
+int als_write_prediction_csv(const char* path, const float* U, int64_t n_users, int64_t ldu, const float* M,
+                             int64_t n_movies, int64_t ldm, int num_features);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFK_ALS_HOST_H */

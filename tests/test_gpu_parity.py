@@ -1,0 +1,198 @@
+"""GPU parity: libcfk_als.so on cuda:0 against the CPU oracle and the committed golden fixtures.
+
+Tolerances (BASELINE.json north star): fp64 parity mode -> factor max-relative error <= 1e-6 (denominator
+floor max(|x|, 1e-12*||row||)) and MSE relative <= 1e-6; fp32 fast mode -> MSE delta <= 1e-3.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, max_rel
+
+pytestmark = pytest.mark.gpu
+
+LAM = 0.05
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _golden(name):
+    return np.load(os.path.join(GOLDEN, f"{name}_k10_n10_p4_seed42_f64.npz"))
+
+
+@pytest.mark.parametrize("name,nm,nu", [("tiny", 426, 302), ("medium", 3590, 2120)])
+def test_f64_parity_vs_golden(cfk, name, nm, nu):
+    """BASELINE configs[0]/[1]: k=10, lambda=0.05, 10 iterations, 4 partitions, fp64 parity mode."""
+    ds = cfk.Dataset.load_netflix(os.path.join(GOLDEN, f"data_sample_{name}.txt"))
+    app = cfk.ALSApp(4, 10, LAM, 10, nm, nu, precision="f64", seed=42).setup(ds)
+    app.run()
+    U, M = app.factors()
+    g = _golden(name)
+    assert max_rel(U, g["U"]) <= 1e-6
+    assert max_rel(M, g["M"]) <= 1e-6
+    assert abs(app.mse() - float(g["mse"])) / float(g["mse"]) <= 1e-6
+
+
+@pytest.mark.parametrize("name,nm,nu", [("tiny", 426, 302), ("medium", 3590, 2120)])
+def test_f32_fast_mode_mse_delta(cfk, name, nm, nu):
+    ds = cfk.Dataset.load_netflix(os.path.join(GOLDEN, f"data_sample_{name}.txt"))
+    app = cfk.ALSApp(4, 10, LAM, 10, nm, nu, precision="f32", seed=42).setup(ds)
+    app.run()
+    g = _golden(name)
+    assert abs(app.mse() - float(g["mse"])) <= 1e-3
+    U, M = app.factors()
+    assert np.linalg.norm(U - g["U"]) / np.linalg.norm(g["U"]) < 1e-3
+
+
+def _one_half(cfk, side, blk, opp_f, k, precision, opp_rows):
+    eng = cfk.ALSEngine(k, precision)
+    eng.use_torch_stream()
+    eng.alloc_factors(1 - side, opp_rows)
+    eng.alloc_factors(side, max(1, blk["n_rows"]))
+    eng.set_block(side, blk["row_ptr"], blk["col"], blk["ratings"], 0, opp_rows)
+    eng.write_factors(1 - side, opp_f)
+    eng.solve_half(side, LAM)
+    out = eng.read_factors(side, 0, blk["n_rows"])
+    eng.close()
+    return out
+
+
+def test_known_answer_systems(cfk):
+    import json
+    for c in json.load(open(os.path.join(GOLDEN, "known_answers.json"))):
+        n, k = c["n"], c["k"]
+        blk = {"row_ptr": np.array([0, n]), "col": np.arange(n, dtype=np.int32), "ratings": np.array(c["r"], np.int16),
+               "n_rows": 1}
+        Y = np.asarray(c["Y"], np.float64)
+        x64 = _one_half(cfk, 0, blk, Y, k, "f64", n)[0]
+        np.testing.assert_allclose(x64, c["x"], rtol=1e-12, atol=1e-13)
+        x32 = _one_half(cfk, 0, blk, Y.astype(np.float32), k, "f32", n)[0]
+        np.testing.assert_allclose(x32, c["x"], rtol=3e-4, atol=3e-5)
+
+
+def _synthetic(cfk, oracle_mod, n_users=3000, n_movies=400, nnz=90_000, seed=11):
+    ds = cfk.Dataset.synthetic_netflix(n_users=n_users, n_movies=n_movies, nnz=nnz, seed=seed, nthreads=8)
+    m, u, r = ds.ratings()
+    return ds, oracle_mod.build_blocks(m, u, r)
+
+
+@pytest.mark.parametrize("k", [1, 5, 10, 16, 17, 31, 32, 33, 48, 63, 64])
+def test_one_half_every_k_vs_oracle(cfk, oracle_mod, k):
+    """Both sides, f64 (VALU path) to 1e-9 and f32 (VALU k<32 / MFMA k>=32) to norm-rel 1e-4."""
+    ds, b = _synthetic(cfk, oracle_mod)
+    rng = np.random.default_rng(k)
+    for side, rows, opp in ((0, b.movie, b.user), (1, b.user, b.movie)):
+        blk = ds.shard_block(side)
+        F = rng.random((len(opp.ids), k))
+        ref = oracle_mod.update_side(rows, F, LAM, "f64")
+        got64 = _one_half(cfk, side, blk, F, k, "f64", len(opp.ids))
+        assert max_rel(got64, ref) <= 1e-9, (side, k)
+        got32 = _one_half(cfk, side, blk, F.astype(np.float32), k, "f32", len(opp.ids))
+        rel = np.linalg.norm(got32 - ref, axis=1) / np.linalg.norm(ref, axis=1)
+        assert rel.max() <= 1e-4, (side, k, rel.max())
+
+
+@pytest.mark.parametrize("chunk", ["4", "64", "256"])
+def test_partial_reduce_split_rows(cfk, oracle_mod, monkeypatch, chunk):
+    """Long rows split into PARTIAL chunks + a REDUCE task give the same solution."""
+    monkeypatch.setenv("ALS_CHUNK", chunk)
+    ds, b = _synthetic(cfk, oracle_mod, n_users=2000, n_movies=150, nnz=60_000, seed=3)
+    for k, prec, tol in ((10, "f64", 1e-9), (64, "f64", 1e-9), (64, "f32", 1e-4), (32, "f32", 1e-4), (10, "f32", 1e-4)):
+        F = np.random.default_rng(1).random((len(b.user.ids), k))
+        ref = oracle_mod.update_side(b.movie, F, LAM, "f64")
+        got = _one_half(cfk, 0, ds.shard_block(0), F.astype(np.float32 if prec == "f32" else np.float64), k, prec,
+                        len(b.user.ids))
+        rel = np.linalg.norm(got - ref, axis=1) / np.linalg.norm(ref, axis=1)
+        assert rel.max() <= tol, (chunk, k, prec, rel.max())
+
+
+def test_valu_and_mfma_paths_agree(cfk, oracle_mod, monkeypatch):
+    ds, b = _synthetic(cfk, oracle_mod)
+    F = np.random.default_rng(2).random((len(b.user.ids), 64)).astype(np.float32)
+    mfma = _one_half(cfk, 0, ds.shard_block(0), F, 64, "f32", len(b.user.ids))
+    monkeypatch.setenv("ALS_FORCE_VALU", "1")
+    valu = _one_half(cfk, 0, ds.shard_block(0), F, 64, "f32", len(b.user.ids))
+    assert np.linalg.norm(mfma - valu) / np.linalg.norm(valu) < 1e-5
+
+
+def test_full_run_k64_f32_mse_vs_oracle(cfk, oracle_mod):
+    ds, b = _synthetic(cfk, oracle_mod)
+    app = cfk.ALSApp(1, 64, LAM, 3, precision="f32", seed=9).setup(ds)
+    app.run()
+    U, M = app.factors()
+    Uo, Mo = oracle_mod.run_als(b, 64, LAM, 3, seed=9, precision="f64")
+    assert abs(app.mse() - oracle_mod.mse(b, Uo, Mo)) <= 1e-3
+    se, cnt = app.sq_error()
+    se_o, cnt_o = oracle_mod.sq_error(b.movie, M.astype(np.float64), U.astype(np.float64))
+    assert cnt == cnt_o and se == pytest.approx(se_o, rel=1e-5)
+
+
+def test_sq_error_reduction_f64(cfk, oracle_mod, tiny_path):
+    ds = cfk.Dataset.load_netflix(tiny_path)
+    app = cfk.ALSApp(4, 10, LAM, 2, precision="f64", seed=42).setup(ds)
+    app.run()
+    U, M = app.factors()
+    m, u, r = oracle_mod.parse_netflix(tiny_path)
+    b = oracle_mod.build_blocks(m, u, r)
+    se_o, cnt_o = oracle_mod.sq_error(b.movie, M, U)
+    for side in ("movie", "user"):
+        se, cnt = app.engine.sq_error(side)
+        assert cnt == cnt_o == 3415 and se == pytest.approx(se_o, rel=1e-12)
+
+
+def test_deterministic_bitwise(cfk, tiny_path):
+    outs = []
+    for _ in range(2):
+        ds = cfk.Dataset.load_netflix(tiny_path)
+        app = cfk.ALSApp(4, 64, LAM, 3, precision="f32", seed=1).setup(ds)
+        app.run()
+        outs.append(app.factors())
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+def test_edge_cases(cfk):
+    # empty block: no-op
+    eng = cfk.ALSEngine(16, "f32")
+    eng.use_torch_stream()
+    eng.alloc_factors(0, 1)
+    eng.alloc_factors(1, 3)
+    eng.set_block(0, np.zeros(1, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int16), 0, 3)
+    eng.solve_half(0, LAM)
+    eng.synchronize()
+    # a zero-degree row (cannot occur in the reference) yields zeros; extreme short ratings stay finite
+    eng.set_block(0, np.array([0, 0, 2], np.int64), np.array([1, 2], np.int32), np.array([-32768, 32767], np.int16), 0, 3)
+    eng.alloc_factors(0, 2)
+    eng.write_factors(1, np.ones((3, 16), np.float32))
+    eng.solve_half(0, LAM)
+    out = eng.read_factors(0)
+    assert np.all(out[0] == 0) and np.all(np.isfinite(out[1]))
+    # out-of-range column indices are rejected on the host (never reach the GPU)
+    from cfk_amd._lib import ALSError
+    with pytest.raises(ALSError, match="ALS_ERR_INVALID_ARGUMENT"):
+        eng.set_block(0, np.array([0, 1], np.int64), np.array([3], np.int32), np.array([1], np.int16), 0, 3)
+    with pytest.raises(ALSError, match="ALS_ERR_STATE"):
+        eng2 = cfk.ALSEngine(16, "f32")
+        eng2.solve_half(0, LAM)
+    eng.close()
+
+
+def test_cli_app_end_to_end(tmp_path, oracle_mod, tiny_path):
+    """als_app (ALSAppRunner CLI) writes the prediction CSV; its MSE matches the f64 oracle run."""
+    import subprocess
+    from conftest import ROOT
+    app = os.path.join(ROOT, "collaborative-filtering-kafka_amd", "build", "als_app")
+    res = subprocess.run([app, "4", "10", "0.05", "10", tiny_path, "426", "302", "--precision", "f64", "--seed", "42",
+                          "--out", str(tmp_path)], capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr
+    csvs = list(tmp_path.glob("prediction_matrix_*"))
+    assert len(csvs) == 1
+    g = _golden("tiny")
+    assert oracle_mod.mse_from_csv(tiny_path, str(csvs[0])) == pytest.approx(float(g["mse"]), rel=1e-6)
+    res = subprocess.run([app, "4", "10", "0.05", "10", tiny_path, "1000", "302"], capture_output=True, text=True)
+    assert res.returncode != 0 and "would wait forever" in res.stderr
