@@ -45,8 +45,12 @@ class ALSApp:
         self.info = [None, None]
 
     # -------------------------------------------------------------------------------------------------
-    def setup(self, ds: Dataset, check_duplicates: bool = True) -> "ALSApp":
-        """Blocks of this rank's shard + factor replicas + U0 (UFeatureInitializer after the EOF barrier)."""
+    def setup(self, ds: Dataset, check_duplicates: bool = True, engine_factory=None) -> "ALSApp":
+        """Blocks of this rank's shard + factor replicas + U0 (UFeatureInitializer after the EOF barrier).
+
+        ``engine_factory(k, precision, device)`` replaces the HIP engine with another object of the same
+        interface; only the multi-rank CPU rehearsal tests (gloo) use it, to exercise the sharding and the
+        all-gather on machines without a GPU. The product path is always the HIP engine."""
         nm, nu, nnz = ds.counts()
         if self.NUM_MOVIES is not None and (nm, nu) != (self.NUM_MOVIES, self.NUM_USERS):
             raise ValueError(f"NUM_MOVIES/NUM_USERS = {self.NUM_MOVIES}/{self.NUM_USERS} but the dataset rates "
@@ -56,8 +60,11 @@ class ALSApp:
             raise ValueError("duplicate (user, movie) pairs: the reference never completes such an entity "
                              "(MFeatureCalculator.java:65)")
         self.ds = ds
-        torch.cuda.set_device(self.device)
-        eng = ALSEngine(self.NUM_FEATURES, self.precision, self.device)
+        if engine_factory is None:
+            torch.cuda.set_device(self.device)
+            eng = ALSEngine(self.NUM_FEATURES, self.precision, self.device)
+        else:
+            eng = engine_factory(self.NUM_FEATURES, self.precision, self.device)
         eng.use_torch_stream()
         for side in (SIDE_MOVIE, SIDE_USER):
             blk = ds.shard_block(side, self.world, self.rank)
@@ -77,8 +84,8 @@ class ALSApp:
             return
         import torch.distributed as dist
         S = self.info[side]["slots_per_shard"]
-        full = self.engine.factors[side]
-        dist.all_gather_into_tensor(full, full[self.rank * S:(self.rank + 1) * S], group=self.group)
+        full = self.engine.factors[side]            # [G*S + 1, kp]: last row = sentinel, not exchanged
+        dist.all_gather_into_tensor(full[:self.world * S], full[self.rank * S:(self.rank + 1) * S], group=self.group)
 
     def movie_half(self):
         """MFeatureCalculator-i over this rank's movies + all-gather (movie-features-i topic)."""
@@ -96,11 +103,11 @@ class ALSApp:
 
     def run(self, iterations: int | None = None) -> float:
         n = self.NUM_ALS_ITERATIONS if iterations is None else iterations
-        torch.cuda.synchronize(self.device)
+        self.engine.synchronize()
         t0 = time.perf_counter()
         for _ in range(n):
             self.iteration()
-        torch.cuda.synchronize(self.device)
+        self.engine.synchronize()
         return time.perf_counter() - t0
 
     # -------------------------------------------------------------------------------------------------
@@ -115,7 +122,7 @@ class ALSApp:
         se, cnt = self.engine.sq_error(SIDE_MOVIE)
         if self.world > 1:
             import torch.distributed as dist
-            t = torch.tensor([se, float(cnt)], dtype=torch.float64, device=f"cuda:{self.device}")
+            t = torch.tensor([se, float(cnt)], dtype=torch.float64, device=self.engine.factors[0].device)
             dist.all_reduce(t, group=self.group)
             se, cnt = float(t[0]), int(t[1])
         return se, cnt

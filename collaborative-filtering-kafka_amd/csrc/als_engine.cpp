@@ -47,6 +47,7 @@ struct Block {
     Task* d_tasks = nullptr;        // FULL + PARTIAL, sorted by work (longest first)
     Task* d_reduce = nullptr;       // REDUCE
     int32_t n_tasks = 0, n_reduce = 0, n_slots = 0;
+    int min_waves = 2;              // MFMA variant occupancy target chosen from the work plan
     double* d_task_se = nullptr;    // per-task squared-error partials
 };
 
@@ -78,6 +79,7 @@ struct als_engine {
     Factors fac[2];
     void* d_partials = nullptr;
     size_t partial_bytes = 0;
+    int min_waves = 0;              // ALS_MFMA_WAVES override of the per-block occupancy choice (0 = auto)
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     std::vector<TimingRec> pending;
@@ -108,14 +110,15 @@ void free_block(Block& b) {
 // Chunk length (entries, multiple of 4) above which a row is split into PARTIAL tasks + a REDUCE task.
 // Aim for enough wave-tasks to fill 256 CUs several times over while keeping partial traffic small.
 int64_t chunk_entries(int64_t nnz_padded) {
+    constexpr int64_t B = cfk::BLOCK_ENTRIES;
     if (const char* env = getenv("ALS_CHUNK")) {
         long v = atol(env);
-        if (v >= 4) return (v + 3) & ~3L;
+        if (v >= 1) return (v + B - 1) / B * B;
     }
     int64_t c = nnz_padded / 24576;
     c = std::max<int64_t>(c, 1024);
     c = std::min<int64_t>(c, 8192);
-    return (c + 3) & ~int64_t(3);
+    return (c + B - 1) / B * B;
 }
 
 }  // namespace
@@ -151,6 +154,7 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
     e->kp = kp;
     e->precision = precision;
     e->path = path;
+    if (const char* env = getenv("ALS_MFMA_WAVES")) e->min_waves = std::max(0, atoi(env));
     hipError_t st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (st != hipSuccess) {
         delete e;
@@ -215,16 +219,18 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
         const int64_t d = row_ptr[i + 1] - row_ptr[i];
         if (d < 0) return fail(ALS_ERR_INVALID_ARGUMENT, "row_ptr not monotone at row %lld", (long long)i);
         if (d > INT32_MAX / 2) return fail(ALS_ERR_UNSUPPORTED, "row %lld has %lld entries", (long long)i, (long long)d);
-        nnz_padded += (d + 3) & ~int64_t(3);
+        nnz_padded += (d + cfk::BLOCK_ENTRIES - 1) / cfk::BLOCK_ENTRIES * cfk::BLOCK_ENTRIES;
     }
     for (int64_t t = 0; t < nnz; ++t)
         if (col_idx[t] < 0 || col_idx[t] >= n_opp_rows)
             return fail(ALS_ERR_INVALID_ARGUMENT, "col_idx[%lld]=%d outside [0, %lld)", (long long)t, col_idx[t],
                         (long long)n_opp_rows);
 
-    // Padded device in-block: every row starts on a multiple of 4 entries (one MFMA sub-step = 4
-    // entries); padding entries carry col = -1 and rating 0 and contribute nothing.
-    std::vector<int32_t> col(nnz_padded, -1);
+    // Padded, block-interleaved device in-block (see cfk::block_position): every row starts on a
+    // 32-entry block; padding entries point at the sentinel zero row (col = n_opp_rows) with rating 0.
+    if ((n_opp_rows + 1) * (int64_t)e->kp * (int64_t)e->elem() > INT32_MAX)
+        return fail(ALS_ERR_UNSUPPORTED, "opposite factor matrix exceeds 2 GiB (32-bit gather offsets)");
+    std::vector<int32_t> col(nnz_padded, (int32_t)n_opp_rows);
     std::vector<float> rat(nnz_padded, 0.f);
     std::vector<int64_t> begin(n_rows + 1);
     {
@@ -233,10 +239,11 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
             begin[i] = o;
             const int64_t b = row_ptr[i], d = row_ptr[i + 1] - b;
             for (int64_t t = 0; t < d; ++t) {
-                col[o + t] = col_idx[b + t];
-                rat[o + t] = (float)ratings[b + t];
+                const int64_t pos = o + cfk::block_position(t);
+                col[pos] = col_idx[b + t];
+                rat[pos] = (float)ratings[b + t];
             }
-            o += (d + 3) & ~int64_t(3);
+            o += (d + cfk::BLOCK_ENTRIES - 1) / cfk::BLOCK_ENTRIES * cfk::BLOCK_ENTRIES;
         }
         begin[n_rows] = o;
     }
@@ -246,22 +253,23 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
     int64_t slots = 0;
     for (int64_t i = 0; i < n_rows; ++i) {
         const int64_t d = row_ptr[i + 1] - row_ptr[i];
-        const int64_t pl = (d + 3) & ~int64_t(3);
         Task t{};
         t.row = (int32_t)i;
         t.ndeg = (int32_t)d;
-        if (pl <= chunk) {
+        if (d <= chunk) {
             t.begin = begin[i];
-            t.nsteps = (int32_t)(pl / 4);
+            t.nsteps = (int32_t)((d + 3) / 4);
+            t.nent = (int32_t)d;
             t.slot = -1;
             t.kind = cfk::TASK_FULL;
             tasks.push_back(t);
         } else {
             const int64_t first = slots;
-            for (int64_t o = 0; o < pl; o += chunk) {
+            for (int64_t o = 0; o < d; o += chunk) {
                 Task p = t;
                 p.begin = begin[i] + o;
-                p.nsteps = (int32_t)(std::min(chunk, pl - o) / 4);
+                p.nsteps = (int32_t)((std::min(chunk, d - o) + 3) / 4);
+                p.nent = (int32_t)std::min(chunk, d - o);
                 p.slot = (int32_t)slots++;
                 p.kind = cfk::TASK_PARTIAL;
                 tasks.push_back(p);
@@ -292,6 +300,10 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
     blk.n_tasks = (int32_t)tasks.size();
     blk.n_reduce = (int32_t)reduce.size();
     blk.n_slots = (int32_t)slots;
+    // Many short tasks (user side: ~200 ratings, one 64x64 solve each) are bound by the solve's VALU work
+    // and gain from a third wave per SIMD; long chunks (movie side) are MFMA-bound and prefer 2 waves
+    // without register spills (measured on the Netflix-shape workload, tools/kbench.py).
+    blk.min_waves = e->min_waves > 0 ? e->min_waves : (nnz_padded < (int64_t)tasks.size() * 1024 ? 3 : 2);
     auto up = [&](void** dst, const void* src, size_t bytes) -> int {
         if (bytes == 0) return ALS_OK;
         hipError_t st = hipMalloc(dst, bytes);
@@ -328,7 +340,7 @@ int als_alloc_factors(als_engine* e, int side, int64_t n_total_rows) {
     Factors& f = e->fac[side];
     if (f.owned) (void)hipFree(f.ptr);
     f = Factors();
-    const size_t bytes = (size_t)std::max<int64_t>(n_total_rows, 1) * e->kp * e->elem();
+    const size_t bytes = (size_t)(n_total_rows + 1) * e->kp * e->elem();   // + sentinel zero row
     hipError_t st = hipMalloc(&f.ptr, bytes);
     if (st != hipSuccess) return fail(ALS_ERR_OUT_OF_MEMORY, "factors hipMalloc(%zu): %s", bytes, hipGetErrorString(st));
     f.owned = true;
@@ -347,6 +359,11 @@ int als_bind_factors(als_engine* e, int side, void* device_ptr, int64_t n_total_
     f.ptr = device_ptr;
     f.n_rows = n_total_rows;
     f.owned = false;
+    // the sentinel row after the last factor row must read as zeros (padding entries gather it)
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipMemsetAsync((char*)device_ptr + (size_t)n_total_rows * e->kp * e->elem(), 0, (size_t)e->kp * e->elem(),
+                           e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
     return ALS_OK;
 }
 
@@ -405,9 +422,9 @@ int als_solve_half(als_engine* e, int side, float lambda) {
     if (b.row_offset + b.n_rows > self.n_rows)
         return fail(ALS_ERR_STATE, "block rows [%lld,%lld) exceed factor rows %lld", (long long)b.row_offset,
                     (long long)(b.row_offset + b.n_rows), (long long)self.n_rows);
-    if (b.n_opp_rows > opp.n_rows)
-        return fail(ALS_ERR_STATE, "block indexes %lld opposite rows, factor matrix has %lld", (long long)b.n_opp_rows,
-                    (long long)opp.n_rows);
+    if (b.n_opp_rows != opp.n_rows)   // the padding entries gather row n_opp_rows: it must be the sentinel
+        return fail(ALS_ERR_STATE, "block was set for %lld opposite rows, the opposite factor matrix has %lld",
+                    (long long)b.n_opp_rows, (long long)opp.n_rows);
     if (!(lambda >= 0.f)) return fail(ALS_ERR_INVALID_ARGUMENT, "lambda must be >= 0");
     HIP_TRY(hipSetDevice(e->device));
     cfk::SolveArgs a{};
@@ -421,6 +438,7 @@ int als_solve_half(als_engine* e, int side, float lambda) {
     a.row_offset = b.row_offset;
     a.partials = e->d_partials;
     a.lambda = lambda;
+    a.sentinel = (int32_t)b.n_opp_rows;
     TimingRec rec{side, {nullptr, nullptr, nullptr}};
     if (e->timing) {
         for (auto& ev : rec.ev) {
@@ -433,12 +451,12 @@ int als_solve_half(als_engine* e, int side, float lambda) {
         }
         HIP_TRY(hipEventRecord(rec.ev[0], e->stream));
     }
-    HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream));
+    HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves));
     if (e->timing) HIP_TRY(hipEventRecord(rec.ev[1], e->stream));
     if (b.n_reduce > 0) {
         a.tasks = b.d_reduce;
         a.n_tasks = b.n_reduce;
-        HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream));
+        HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves));
     }
     if (e->timing) {
         HIP_TRY(hipEventRecord(rec.ev[2], e->stream));
@@ -465,6 +483,7 @@ int als_sq_error(als_engine* e, int side, double* sum_sq_error, int64_t* count) 
     a.self = self.ptr;
     a.row_offset = b.row_offset;
     a.task_se = b.d_task_se;
+    a.sentinel = (int32_t)b.n_opp_rows;
     HIP_TRY(cfk::launch_sq_error(e->precision, e->kp, a, e->stream));
     std::vector<double> se(b.n_tasks);
     if (b.n_tasks > 0)

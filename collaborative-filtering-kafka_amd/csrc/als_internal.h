@@ -15,14 +15,28 @@ namespace cfk {
 //   kind REDUCE  : sum partial slots [slot, slot + nsteps) of row `row` in fixed order, then solve + store.
 enum TaskKind : int32_t { TASK_FULL = 0, TASK_PARTIAL = 1, TASK_REDUCE = 2 };
 
+// Device in-block layout: each row is padded to whole blocks of BLOCK_ENTRIES = 32 entries; padding entries
+// hold col = n_opp_rows (the sentinel zero row kept after the last factor row) and rating 0, so they add
+// nothing and need no masking in the kernels. Entry e of a
+// row is consumed by sub-step t = e / 4 (one MFMA K=4 step) in lane group g = e % 4; inside a block the
+// entries are stored group-major ([g][t], t < 8) so that one lane fetches the column indices of its 8
+// sub-steps with two 16-byte loads.
+constexpr int BLOCK_SUBSTEPS = 8;
+constexpr int BLOCK_ENTRIES = 4 * BLOCK_SUBSTEPS;
+__host__ __device__ constexpr int64_t block_position(int64_t e) {
+    const int64_t blk = e / BLOCK_ENTRIES, w = e % BLOCK_ENTRIES;
+    return blk * BLOCK_ENTRIES + (w % 4) * BLOCK_SUBSTEPS + w / 4;
+}
+
 struct alignas(16) Task {
-    int64_t begin;   // entry offset into the padded col/rating arrays (multiple of 4)
-    int32_t nsteps;  // FULL/PARTIAL: number of 4-entry sub-steps; REDUCE: number of partial slots
+    int64_t begin;   // entry offset into the padded col/rating arrays (multiple of BLOCK_ENTRIES)
+    int32_t nsteps;  // FULL/PARTIAL: sub-steps holding real entries (ceil(n/4)); the task spans
+                     // ceil(nsteps / BLOCK_SUBSTEPS) blocks. REDUCE: number of partial slots
     int32_t row;     // local row of the block (factor row = row_offset + row)
     int32_t slot;    // PARTIAL: slot written; REDUCE: first slot read; FULL: -1
     int32_t ndeg;    // true in-block size n_j (lambda * n_j * I, MFeatureCalculator.java:92-95)
     int32_t kind;
-    int32_t pad;
+    int32_t nent;    // FULL/PARTIAL: real entries in this task's range (logical indices [0, nent))
 };
 static_assert(sizeof(Task) == 32, "Task layout");
 
@@ -37,6 +51,7 @@ struct SolveArgs {
     int64_t row_offset;     // first factor row of this block
     void* partials;         // partial-slot workspace
     float lambda;
+    int32_t sentinel;       // index of the opposite side's all-zero sentinel row (= n_opp_rows)
 };
 
 struct SqErrArgs {
@@ -48,12 +63,14 @@ struct SqErrArgs {
     const void* self;
     int64_t row_offset;
     double* task_se;        // [n_tasks]
+    int32_t sentinel;
 };
 
 enum class Path : int { VALU = 0, MFMA = 1 };
 
 // Launch helpers (defined in als_kernels.hip). Return hipSuccess or the launch error.
-hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s);
+// min_waves: occupancy target (waves per SIMD) of the MFMA variant (__launch_bounds__ second argument).
+hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, int min_waves);
 hipError_t launch_sq_error(int precision, int kp, const SqErrArgs& a, hipStream_t s);
 // Per-lane accumulator words (elements of the engine precision) of one partial slot: nacc * 64.
 int partial_words_per_lane(int precision, int kp, Path path);

@@ -15,9 +15,11 @@
 //        LDS, no shuffles). RHS is a per-lane VALU FMA, reduced across the 4 groups at the end.
 //   VALU (fp32 KP = 16, all fp64): 64 gathered rows are staged in LDS (coalesced 16-B vector loads), then
 //        each lane accumulates KP*KP/64 Gram entries of one row from LDS broadcasts.
-// Solve: the Gram is canonicalised into a per-wave LDS matrix G[KP][KP+1]; lane j loads row j, adds
-// lambda*n_j to the diagonal, and runs a right-looking Cholesky with L's column broadcast through LDS,
-// then forward / backward substitution with v_readlane broadcasts (L transposed once through LDS).
+// Solve: the Gram is canonicalised into a per-wave packed lower triangle in LDS (KP*(KP+1)/2 words); lane j
+// loads row j, adds lambda*n_j to the diagonal, and runs a right-looking Cholesky: the two look-ahead
+// columns of every step are broadcast with v_readlane (so the pivot chain never waits on LDS) and the bulk
+// of L's column goes through a KP-word LDS vector read back 16 B at a time; forward substitution is fused
+// into the factorisation; L is transposed once through the packed triangle for the backward substitution.
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -60,12 +62,25 @@ __device__ __forceinline__ double bcast(double v, int src) {
     return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// Compile-time loop: f(std::integral_constant<int, i>) for i in [B, E). Every index derived from i is a
+// constant expression, so register arrays are never indexed dynamically (no scratch).
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
 // Fresh copy of a per-lane value the optimizer cannot see through: stops LLVM from CSE-ing the 3*KP
 // lane-vs-step comparisons of the unrolled solve into live SGPR masks (which spill).
 __device__ __forceinline__ int opaque(int v) {
     asm volatile("" : "+v"(v));
     return v;
 }
+// Materialise a value here: keeps LLVM from sinking a step's rank-1 updates into deferred FMA chains at the
+// next use (MachineSink ignores sched_barrier), which multiplies live registers in the unrolled solve.
+__device__ __forceinline__ void pin(float& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(double& v) { asm volatile("" : "+v"(v)); }
 
 __device__ __forceinline__ Task load_task(const Task* p) {
     Task t = *p;
@@ -85,8 +100,7 @@ __host__ __device__ constexpr int round16(int b) { return (b + 15) & ~15; }
 
 template <class T, int KP, Path P>
 struct WaveLds {
-    static constexpr int LD = KP + 1;                                 // conflict-free row and column reads
-    static constexpr int G_BYTES = round16(KP * LD * (int)sizeof(T));
+    static constexpr int G_BYTES = round16(KP * (KP + 1) / 2 * (int)sizeof(T));   // packed lower triangle
     static constexpr int STAGE_BYTES = (P == Path::VALU) ? round16(RSTAGE * KP * (int)sizeof(T)) : 0;
     static constexpr int MAIN_BYTES = G_BYTES > STAGE_BYTES ? G_BYTES : STAGE_BYTES;   // staging aliases G
     static constexpr int RHS_OFF = MAIN_BYTES;
@@ -99,13 +113,34 @@ struct WaveLds {
 // ---------------------------------------------------------------------------------------------------
 // In-wave Cholesky solve (lane j = row j), shared by both paths
 // ---------------------------------------------------------------------------------------------------
+// packed lower-triangular index (c <= r)
+__host__ __device__ constexpr int tri(int r, int c) { return r * (r + 1) / 2 + c; }
+
+// Pivot of one Cholesky step: d = sqrt(a), dinv = 1/sqrt(a). fp32 uses v_rsq_f32 (1 ulp; the fp32 fast mode
+// is held to an MSE bound), fp64 keeps correctly rounded sqrt and division for the 1e-6 parity mode.
+__device__ __forceinline__ void pivot(float a, float& d, float& dinv) {
+    dinv = __builtin_amdgcn_rsqf(a);
+    d = a * dinv;
+}
+__device__ __forceinline__ void pivot(double a, double& d, double& dinv) {
+    d = sqrt(a);
+    dinv = 1.0 / d;
+}
+
+// Lane j owns row j of A and computes row j of L. A lane never needs an entry right of its diagonal
+// (i > j): those registers may hold anything finite, which makes the solve nearly select-free -- every
+// step runs the same instructions on all lanes; only the per-step uniform results (1/L[p][p], the forward
+// and backward solution components) are dropped into lane p with one compare + select; the row load and
+// the transposition are unpredicated LDS accesses.
 template <class T, int KP>
-__device__ __forceinline__ void solve_store(T* G, const T* rhs_l, T* bc, const Task& tk, const SolveArgs& a,
+__device__ __forceinline__ void solve_store(T* P, const T* rhs_l, T* bc, const Task& tk, const SolveArgs& a,
                                             int lane) {
-    constexpr int LD = KP + 1;
+    using BV = typename Vec16<T>::type;
+    constexpr int BN = Vec16<T>::N;
+    static_assert(KP <= 64, "one row per lane");
     const int j = lane;
     const bool act = j < KP;
-    const int jr = act ? j : 0;
+    const int jr = act ? j : KP - 1;
     T* out = (T*)a.out + (a.row_offset + tk.row) * (int64_t)KP;
 
     if (tk.ndeg == 0) {   // cannot occur in the reference (entities exist only once rated); defined as 0
@@ -113,71 +148,113 @@ __device__ __forceinline__ void solve_store(T* G, const T* rhs_l, T* bc, const T
         return;
     }
 
+    // A + lambda * (n * I) on the packed diagonal: fp32 mirrors add(A, lambda, n*I)
+    // (MFeatureCalculator.java:91-95) -> A[j][j] + lambda*(float)n; padded features get an identity row.
+    const T reg = (T)a.lambda * (T)tk.ndeg;
+    const int rowbase = tri(jr, 0);
+    if (act) {
+        const T dd = P[rowbase + jr];
+        P[rowbase + jr] = (j < a.k) ? dd + reg : T(1);
+    }
+    wave_sync();
+    // Row j, entries 0..KP-1 read straight through the packed triangle: entries i > j land in the next
+    // rows' storage (finite, never used). rowbase + i <= tri(KP-1, 0) + KP-1: always in bounds.
     T av[KP];
 #pragma unroll
-    for (int i = 0; i < KP; ++i) av[i] = G[jr * LD + i];
+    for (int i = 0; i < KP; ++i) av[i] = P[rowbase + i];
     T y = act ? rhs_l[jr] : T(0);
 
-    // A + lambda * (n * I): fp32 mirrors add(A, lambda, n*I) (MFeatureCalculator.java:91-95) -> lambda*(float)n
-    const T reg = (T)a.lambda * (T)tk.ndeg;
-    const bool real_feature = j < a.k;
-#pragma unroll
-    for (int i = 0; i < KP; ++i) {
-        const int jo = opaque(j);
-        if (i == jo) av[i] = real_feature ? av[i] + reg : T(1);   // padded features: identity rows
+    T dinv = T(0), z = T(0);     // lane p: 1/L[p][p] and the forward solution z_p
+    T rs_cur, l;
+    {
+        T d;
+        pivot(bcast(av[0], 0), d, rs_cur);
+        l = av[0] * rs_cur;       // lane 0 gets ~L[0][0]; lanes > 0 L[j][0]
+        av[0] = l;
     }
-
-    // Right-looking Cholesky: after step p lane j holds L[j][0..p] in av[0..p]. Column p of L is
-    // broadcast through a KP-word LDS vector read back 16 B at a time; sched_barriers keep the compiler
-    // from hoisting later steps' reads (which would blow the register budget).
-    using BV = typename Vec16<T>::type;
-    constexpr int BN = Vec16<T>::N;
-    T dinv = T(0);
-#pragma unroll
-    for (int p = 0; p < KP; ++p) {
-        const int jo = opaque(j);
-        const T d = sqrt(bcast(av[p], p));
-        const T id = T(1) / d;
-        const T l = (jo > p) ? av[p] * id : ((jo == p) ? d : T(0));
-        av[p] = l;
-        dinv = (jo == p) ? id : dinv;
-        if (act) bc[j] = l;
-        wave_sync();
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = ((p + 1) / BN) * BN; q < KP; q += BN) {
-            const BV b = *(const BV*)(bc + q);
-#pragma unroll
-            for (int c = 0; c < BN; ++c)
-                if (q + c > p) av[q + c] -= b[c] * l;
-            if ((q / BN) % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+    static_for<0, KP>([&](auto P_) {
+        constexpr int p = decltype(P_)::value;
+        // forward substitution with column p: z_p = y_p / L[p][p]; y_j -= L[j][p] z_p (lanes > p; lane p
+        // and lanes < p update registers they no longer need)
+        const T zp = bcast(y, p) * rs_cur;
+        const bool me = opaque(j) == p;
+        z = me ? zp : z;
+        dinv = me ? rs_cur : dinv;
+        y -= l * zp;
+        // look-ahead columns p+1, p+2 through v_readlane: the next pivots never wait on LDS
+        if constexpr (p + 1 < KP) av[p + 1] -= bcast(l, p + 1) * l;
+        if constexpr (p + 2 < KP) av[p + 2] -= bcast(l, p + 2) * l;
+        // next pivot (p+1): lane p+1 gets ~L[p+1][p+1], lanes > p+1 L[j][p+1]
+        T l_next = T(0), rs_next = T(0);
+        if constexpr (p + 1 < KP) {
+            T d;
+            pivot(bcast(av[p + 1], p + 1), d, rs_next);
+            l_next = av[p + 1] * rs_next;
+            av[p + 1] = l_next;
         }
-        wave_sync();
+        // bulk trailing update of columns >= p+3: L[i][p] broadcast through LDS, 16 B per read,
+        // double-buffered so that reads of the next chunk are in flight under this chunk's FMAs
+        if constexpr (p + 3 < KP) {
+            wave_sync();
+            if (act) bc[j] = l;
+            wave_sync();
+            constexpr int CH = 4;                              // 16-B vectors per chunk
+            constexpr int q0 = ((p + 3) / BN) * BN;
+            constexpr int nvec = (KP - q0) / BN;
+            constexpr int nch = (nvec + CH - 1) / CH;
+            BV buf[2][CH];
+            static_for<0, (CH < nvec ? CH : nvec)>([&](auto V_) {
+                constexpr int v = decltype(V_)::value;
+                buf[0][v] = *(const BV*)(bc + q0 + v * BN);
+            });
+            static_for<0, nch>([&](auto C_) {
+                constexpr int c = decltype(C_)::value;
+                if constexpr (c + 1 < nch) {
+                    static_for<0, CH>([&](auto V_) {
+                        constexpr int v = decltype(V_)::value;
+                        if constexpr ((c + 1) * CH + v < nvec)
+                            buf[(c + 1) & 1][v] = *(const BV*)(bc + q0 + ((c + 1) * CH + v) * BN);
+                    });
+                }
+                static_for<0, CH>([&](auto V_) {
+                    constexpr int v = decltype(V_)::value;
+                    if constexpr (c * CH + v < nvec) {
+                        static_for<0, BN>([&](auto E_) {
+                            constexpr int e = decltype(E_)::value;
+                            constexpr int i = q0 + (c * CH + v) * BN + e;
+                            if constexpr (i >= p + 3) av[i] -= buf[c & 1][v][e] * l;
+                        });
+                    }
+                });
+                __builtin_amdgcn_sched_barrier(0);
+            });
+        }
+        static_for<p + 1, KP>([&](auto I_) { pin(av[decltype(I_)::value]); });
+        l = l_next;
+        rs_cur = rs_next;
         __builtin_amdgcn_sched_barrier(0);
-    }
-    // Forward substitution L y = b (lane j owns row j of L).
-#pragma unroll
-    for (int p = 0; p < KP; ++p) {
-        const int jo = opaque(j);
-        const T yp = bcast(y, p) * bcast(dinv, p);
-        y = (jo == p) ? yp : ((jo > p) ? y - av[p] * yp : y);
-    }
-    // Transpose L through LDS: lane j then owns column j (av[i] = L[i][j]).
+    });
+    // Transpose L through the packed triangle: lane j writes its row into ITS OWN segment only -- the
+    // right-of-diagonal (garbage) entries i > j go to min(i, j) = the lane's diagonal slot, written before
+    // the valid diagonal (descending i; same address, so program order holds). Then lane j reads column j.
+    wave_sync();
     if (act) {
 #pragma unroll
-        for (int i = 0; i < KP; ++i) G[j * LD + i] = av[i];
+        for (int i = KP - 1; i >= 0; --i) P[rowbase + min(i, jr)] = av[i];
     }
     wave_sync();
 #pragma unroll
-    for (int i = 0; i < KP; ++i) av[i] = G[i * LD + jr];
-    // Backward substitution L^T x = y.
+    for (int i = 0; i < KP; ++i) av[i] = P[tri(i, 0) + jr];   // = L[i][j] for i >= j; garbage above
+    // Backward substitution L^T x = z (column-oriented, p descending): x_p = z'_p / L[p][p],
+    // z'_j -= L[p][j] x_p for j < p.
+    T x = T(0);
 #pragma unroll
     for (int p = KP - 1; p >= 0; --p) {
-        const int jo = opaque(j);
-        const T xp = bcast(y, p) * bcast(dinv, p);
-        y = (jo == p) ? xp : ((jo < p) ? y - av[p] * xp : y);
+        const T xp = bcast(z, p) * bcast(dinv, p);
+        x = (opaque(j) == p) ? xp : x;
+        z -= av[p] * xp;
     }
-    if (act) out[j] = (j < a.k) ? y : T(0);
+    if (act) out[j] = (j < a.k) ? x : T(0);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -194,8 +271,8 @@ struct MfmaAcc {
 template <int C>
 __host__ __device__ constexpr int tile_index(int b1, int b2) { return b1 * C - (b1 * (b1 - 1)) / 2 + (b2 - b1); }
 
-template <int KP>
-__global__ __launch_bounds__(256) void als_solve_mfma(SolveArgs a) {
+template <int KP, int MINW>
+__global__ __launch_bounds__(256, MINW) void als_solve_mfma(SolveArgs a) {
     constexpr int C = KP / 16;
     using Acc = MfmaAcc<C>;
     using VT = typename VecC<C>::type;
@@ -231,58 +308,69 @@ __global__ __launch_bounds__(256) void als_solve_mfma(SolveArgs a) {
             for (int c = 0; c < C; ++c) acc.rhs[c] += src[(Acc::NT * 4 + c) * 64];
         }
     } else {
+        // Gather pipeline over blocks of B = 8 sub-steps (32 entries, layout [g][t], see block_position):
+        // lane (g, j) loads the 8 column indices / ratings of its group with two 16-B loads, issued one
+        // block ahead of that block's gathers, which are issued one block ahead of their MFMAs. The loop
+        // body is branch-free, so vmcnt retires in program order with 8 gathers (8 KB per wave) still in
+        // flight under each block's 80 MFMAs.
+        constexpr int B = BLOCK_SUBSTEPS;
         const float* opp = (const float*)a.opp;
         const int n = tk.nsteps;
-        const int32_t* cp = a.col + tk.begin + g;
-        const float* rp = a.rat + tk.begin + g;
-        constexpr int U = 4;
-        int idx_c[U], idx_n[U];
-        float r_c[U], r_n[U];
-        VT y_c[U], y_n[U];
-        auto load_idx = [&](int t0, int (&idx)[U], float (&r)[U]) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int t = t0 + u;
-                idx[u] = (t < n) ? cp[4 * t] : -1;
-                r[u] = (t < n) ? rp[4 * t] : 0.f;
-            }
+        const int nblk = (n + B - 1) / B;
+        const int32_t* cb = a.col + tk.begin + g * B;
+        const float* rb = a.rat + tk.begin + g * B;
+        typedef int i32x4 __attribute__((ext_vector_type(4)));
+        struct Idx { i32x4 i[2]; f32x4 r[2]; };
+        auto load_idx = [&](int blk, Idx& x) {
+            const int32_t* c = cb + (int64_t)blk * BLOCK_ENTRIES;
+            const float* r = rb + (int64_t)blk * BLOCK_ENTRIES;
+            x.i[0] = *(const i32x4*)c;
+            x.i[1] = *(const i32x4*)(c + 4);
+            x.r[0] = *(const f32x4*)r;
+            x.r[1] = *(const f32x4*)(r + 4);
         };
-        auto gather = [&](const int (&idx)[U], VT (&y)[U]) {
+        // unconditional: padding entries index the sentinel zero row; 32-bit byte offsets (host-checked)
+        const char* obase = (const char*)(opp + C * j);
+        auto gather = [&](const Idx& x, VT (&y)[B]) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int id = idx[u] < 0 ? 0 : idx[u];
-                const VT v = *(const VT*)(opp + (int64_t)id * KP + C * j);
-                y[u] = idx[u] < 0 ? VT(0.f) : v;
-            }
+            for (int t = 0; t < B; ++t)
+                y[t] = *(const VT*)(obase + (uint32_t)x.i[t >> 2][t & 3] * (uint32_t)(KP * sizeof(float)));
         };
-        load_idx(0, idx_c, r_c);
-        gather(idx_c, y_c);
-        load_idx(U, idx_n, r_n);
-        for (int t0 = 0; t0 < n; t0 += U) {
-            gather(idx_n, y_n);                 // next block's rows in flight under this block's MFMAs
-            int idx_nn[U];
-            float r_nn[U];
-            load_idx(t0 + 2 * U, idx_nn, r_nn);
+        auto mfma_step = [&](const VT& y, float r) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (t0 + u < n) {               // wave-uniform
+            for (int b1 = 0; b1 < C; ++b1)
 #pragma unroll
-                    for (int b1 = 0; b1 < C; ++b1)
+                for (int b2 = b1; b2 < C; ++b2)
+                    acc.g[tile_index<C>(b1, b2)] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        y[b1], y[b2], acc.g[tile_index<C>(b1, b2)], 0, 0, 0);
 #pragma unroll
-                        for (int b2 = b1; b2 < C; ++b2)
-                            acc.g[tile_index<C>(b1, b2)] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                                y_c[u][b1], y_c[u][b2], acc.g[tile_index<C>(b1, b2)], 0, 0, 0);
+            for (int c = 0; c < C; ++c) acc.rhs[c] += r * y[c];
+        };
+        if (nblk > 0) {
+            Idx x_c, x_n;
+            VT y_c[B], y_n[B];
+            load_idx(0, x_c);
+            load_idx(nblk > 1 ? 1 : 0, x_n);
+            gather(x_c, y_c);
+            for (int b = 0; b + 1 < nblk; ++b) {
+                Idx x_nn;
+                load_idx(b + 2 < nblk ? b + 2 : nblk - 1, x_nn);   // clamped: always a valid address
+                gather(x_n, y_n);
+                // keep the prefetch above the MFMAs: without this the scheduler sinks the gathers below
+                // them (saving registers) and every block waits out a full memory latency
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int c = 0; c < C; ++c) acc.rhs[c] += r_c[u] * y_c[u][c];
-                }
+                for (int t = 0; t < B; ++t) mfma_step(y_c[t], x_c.r[t >> 2][t & 3]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int t = 0; t < B; ++t) y_c[t] = y_n[t];
+                x_c = x_n;
+                x_n = x_nn;
             }
+            const int last = n - (nblk - 1) * B;     // sub-steps with real entries in the last block
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                y_c[u] = y_n[u];
-                r_c[u] = r_n[u];
-                idx_n[u] = idx_nn[u];
-                r_n[u] = r_nn[u];
-            }
+            for (int t = 0; t < B; ++t)
+                if (t < last) mfma_step(y_c[t], x_c.r[t >> 2][t & 3]);   // wave-uniform
         }
     }
 
@@ -297,8 +385,9 @@ __global__ __launch_bounds__(256) void als_solve_mfma(SolveArgs a) {
         return;
     }
 
-    // Canonicalise: tile (b1,b2) lane (g,j) reg r holds G[C*(4g+r)+b1][C*j+b2]; mirror off-diagonal tiles.
-    constexpr int LD = KP + 1;
+    // Canonicalise into the packed lower triangle: tile (b1,b2) lane (g,j) reg r holds G[C*(4g+r)+b1][C*j+b2];
+    // every unordered pair {row, col} occurs exactly once over the b1 <= b2 tiles (both orders inside a
+    // diagonal tile, where only row >= col is stored).
 #pragma unroll
     for (int b1 = 0; b1 < C; ++b1)
 #pragma unroll
@@ -307,8 +396,8 @@ __global__ __launch_bounds__(256) void als_solve_mfma(SolveArgs a) {
             for (int r = 0; r < 4; ++r) {
                 const float v = acc.g[tile_index<C>(b1, b2)][r];
                 const int row = C * (4 * g + r) + b1, col = C * j + b2;
-                G[row * LD + col] = v;
-                if (b1 != b2) G[col * LD + row] = v;
+                if (row >= col) G[tri(row, 0) + col] = v;
+                else if (b1 != b2) G[tri(col, 0) + row] = v;
             }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
@@ -363,10 +452,10 @@ __global__ __launch_bounds__(256) void als_solve_valu(SolveArgs a) {
         }
     } else {
         const T* opp = (const T*)a.opp;
-        const int n = tk.nsteps * 4;
+        const int n = (tk.nsteps + BLOCK_SUBSTEPS - 1) / BLOCK_SUBSTEPS * BLOCK_ENTRIES;   // task span
         for (int base = 0; base < n; base += RSTAGE) {
             const int e = base + lane;
-            int idx = -1;
+            int idx = a.sentinel;
             T r = T(0);
             if (e < n) {
                 idx = a.col[tk.begin + e];
@@ -379,9 +468,8 @@ __global__ __launch_bounds__(256) void als_solve_valu(SolveArgs a) {
             for (int q = 0; q < V; ++q) {       // RSTAGE * V vectors, 64 per instruction
                 const int pair = q * 64 + lane;
                 const int t = pair / V, v = pair % V;
-                const int id = sidx[t];
-                const VT val = *(const VT*)(opp + (int64_t)(id < 0 ? 0 : id) * KP + v * VN);
-                *(VT*)(stage + t * KP + v * VN) = id < 0 ? VT(T(0)) : val;
+                const int id = sidx[t];   // padding entries gather the sentinel zero row
+                *(VT*)(stage + t * KP + v * VN) = *(const VT*)(opp + (int64_t)id * KP + v * VN);
             }
             wave_sync();
             const int nt = (n - base) < RSTAGE ? (n - base) : RSTAGE;
@@ -403,9 +491,9 @@ __global__ __launch_bounds__(256) void als_solve_valu(SolveArgs a) {
         return;
     }
 
-    constexpr int LD = KP + 1;
 #pragma unroll
-    for (int e = 0; e < E; ++e) G[arow * LD + c0 + e] = acc[e];
+    for (int e = 0; e < E; ++e)
+        if (c0 + e <= arow) G[tri(arow, 0) + c0 + e] = acc[e];   // packed lower triangle
     if (lane % LPR == 0) rhs_l[arow] = rhs;
     wave_sync();
     solve_store<T, KP>(G, rhs_l, bc, tk, a, lane);
@@ -428,23 +516,26 @@ __global__ __launch_bounds__(256) void als_sq_error_kernel(SqErrArgs a) {
     const T* self = (const T*)a.self + (a.row_offset + tk.row) * (int64_t)KP;
     const T* opp = (const T*)a.opp;
     const VT x = *(const VT*)(self + v * VN);
-    const int n = tk.nsteps * 4;
+    const int n = (tk.nsteps + BLOCK_SUBSTEPS - 1) / BLOCK_SUBSTEPS * BLOCK_ENTRIES;   // task span
     double se = 0.0;
     for (int base = 0; base < n; base += EPS) {
         const int e = base + es;
-        int idx = -1;
+        int idx = a.sentinel;
         float r = 0.f;
         if (e < n) {
             idx = a.col[tk.begin + e];
             r = a.rat[tk.begin + e];
         }
-        const VT y = *(const VT*)(opp + (int64_t)(idx < 0 ? 0 : idx) * KP + v * VN);
+        const VT y = *(const VT*)(opp + (int64_t)idx * KP + v * VN);
         T dot = T(0);
 #pragma unroll
         for (int c = 0; c < VN; ++c) dot += x[c] * y[c];
 #pragma unroll
         for (int m = 1; m < LPE; m <<= 1) dot += __shfl_xor(dot, m);
-        if (v == 0 && idx >= 0) {
+        // logical entry index of physical position e (block_position inverse): skip the padding
+        const int w = e % BLOCK_ENTRIES;
+        const int logical = e - w + (w % BLOCK_SUBSTEPS) * 4 + w / BLOCK_SUBSTEPS;
+        if (v == 0 && e < n && logical < tk.nent) {
             const double d = (double)r - (double)dot;
             se += d * d;
         }
@@ -456,7 +547,7 @@ __global__ __launch_bounds__(256) void als_sq_error_kernel(SqErrArgs a) {
 
 int blocks_for(int n_tasks) { return (n_tasks + WAVES - 1) / WAVES; }
 
-template <class T, int KP, Path P>
+template <class T, int KP, Path P, int MINW = 1>
 hipError_t launch_solve_t(const SolveArgs& a, hipStream_t s) {
     if (a.n_tasks <= 0) return hipSuccess;
     constexpr int bytes = WAVES * WaveLds<T, KP, P>::BYTES;
@@ -464,12 +555,12 @@ hipError_t launch_solve_t(const SolveArgs& a, hipStream_t s) {
         static_assert(std::is_same<T, float>::value, "MFMA path is fp32");
         static bool attr = false;
         if (!attr) {
-            hipError_t e = hipFuncSetAttribute((const void*)als_solve_mfma<KP>,
+            hipError_t e = hipFuncSetAttribute((const void*)als_solve_mfma<KP, MINW>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
             if (e != hipSuccess) return e;
             attr = true;
         }
-        als_solve_mfma<KP><<<blocks_for(a.n_tasks), 256, bytes, s>>>(a);
+        als_solve_mfma<KP, MINW><<<blocks_for(a.n_tasks), 256, bytes, s>>>(a);
     } else {
         static bool attr = false;
         if (!attr) {
@@ -508,11 +599,12 @@ int partial_words_per_lane(int precision, int kp, Path path) {
     return kp * kp / 64 + 1;
 }
 
-hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s) {
+hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, int min_waves) {
     if (precision == 0) {
         if (path == Path::MFMA) {
-            if (kp == 32) return launch_solve_t<float, 32, Path::MFMA>(a, s);
-            if (kp == 64) return launch_solve_t<float, 64, Path::MFMA>(a, s);
+            if (kp == 32) return launch_solve_t<float, 32, Path::MFMA, 2>(a, s);
+            if (kp == 64 && min_waves >= 3) return launch_solve_t<float, 64, Path::MFMA, 3>(a, s);
+            if (kp == 64) return launch_solve_t<float, 64, Path::MFMA, 2>(a, s);
         } else {
             if (kp == 16) return launch_solve_t<float, 16, Path::VALU>(a, s);
             if (kp == 32) return launch_solve_t<float, 32, Path::VALU>(a, s);

@@ -196,16 +196,18 @@ class ALSEngine:
              ptr(c, ctypes.c_int32), ptr(r, ctypes.c_int16))
 
     def bind_factors(self, side, tensor: torch.Tensor):
+        """Bind a [n_rows + 1, kp] tensor: rows [0, n_rows) are the factors, the last row is the engine's
+        all-zero sentinel (gathered by in-block padding entries; never written)."""
         side = _side(side)
         if tensor.dtype != self.dtype or tensor.dim() != 2 or tensor.shape[1] != self.kp or not tensor.is_contiguous():
-            raise ValueError(f"factor tensor must be contiguous [n, {self.kp}] {self.dtype}")
+            raise ValueError(f"factor tensor must be contiguous [n + 1, {self.kp}] {self.dtype}")
         if tensor.device.type != "cuda":
             raise ValueError("factor tensor must live on the GPU")
-        call("als_bind_factors", self._h, side, ctypes.c_void_p(tensor.data_ptr()), tensor.shape[0])
+        call("als_bind_factors", self._h, side, ctypes.c_void_p(tensor.data_ptr()), tensor.shape[0] - 1)
         self.factors[side] = tensor
 
     def alloc_factors(self, side, n_rows: int) -> torch.Tensor:
-        t = torch.zeros((max(n_rows, 1), self.kp), dtype=self.dtype, device=f"cuda:{self.device}")
+        t = torch.zeros((n_rows + 1, self.kp), dtype=self.dtype, device=f"cuda:{self.device}")
         self.bind_factors(side, t)
         return t
 
@@ -216,7 +218,7 @@ class ALSEngine:
     def read_factors(self, side, row0: int = 0, n_rows: int | None = None) -> np.ndarray:
         side = _side(side)
         if n_rows is None:
-            n_rows = self.factors[side].shape[0] - row0
+            n_rows = self.factors[side].shape[0] - 1 - row0
         out = np.zeros((n_rows, self.k), self.np_dtype)
         call("als_read_factors", self._h, side, row0, n_rows, out.ctypes.data_as(ctypes.c_void_p), self.k)
         return out

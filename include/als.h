@@ -73,10 +73,13 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
                   const int64_t* row_ptr, const int32_t* col_idx, const int16_t* ratings);
 
 /* ---- factor matrices (device resident) ---------------------------------------------------------- */
-/* Engine-owned buffer of n_total_rows x stride elements (zeroed). */
+/* Engine-owned buffer of n_total_rows x stride elements (zeroed), plus one hidden all-zero sentinel row
+ * after the last row (in-block padding entries gather it instead of being masked). */
 int als_alloc_factors(als_engine* e, int side, int64_t n_total_rows);
-/* Caller-owned device buffer (e.g. a torch tensor), row stride = als_factor_stride(e), padding columns
- * must be zero. Lets a collective (RCCL all-gather) write straight into the matrix the engine reads. */
+/* Caller-owned device buffer (e.g. a torch tensor) of n_total_rows + 1 rows, row stride =
+ * als_factor_stride(e), padding columns zero; the engine zeroes row n_total_rows (the sentinel) here and
+ * never writes it, so callers must not either. Lets a collective (RCCL all-gather) write straight into the
+ * matrix the engine reads. */
 int als_bind_factors(als_engine* e, int side, void* device_ptr, int64_t n_total_rows);
 int als_factors_device_ptr(const als_engine* e, int side, void** device_ptr, int64_t* n_total_rows);
 /* Host <-> device copies of rows [row0, row0+n_rows) with a host row stride of src_ld/dst_ld elements
