@@ -79,9 +79,13 @@ def cpu_baseline(ds, k, lam, seconds, threads):
             got.append(r)
         return t, min(got)
 
-    t_probe, r_probe = timed(50_000)
-    target = int(max(50_000, min(5e7, r_probe * seconds / max(t_probe, 1e-3))))
+    target = 200_000
     t, r = timed(target)
+    for _ in range(4):                      # grow the sample until it is ~`seconds` of CPU work
+        if t >= 0.7 * seconds or target >= ds.nnz // 2:
+            break
+        target = int(min(ds.nnz // 2, target * seconds / max(t, 1e-3)))
+        t, r = timed(target)
     return {"value": r / t, "unit": "ratings/s", "cores": threads, "kind": "port",
             "sample": f"oracle f32 (Java-float EJML-order restatement) on random rows of both halves, "
                       f"{r} ratings per half ({r / ds.nnz * 100:.2f}% of a half), {t:.1f} s, {threads} threads"}
