@@ -303,7 +303,7 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
     // Many short tasks (user side: ~200 ratings, one 64x64 solve each) are bound by the solve's VALU work
     // and gain from a third wave per SIMD; long chunks (movie side) are MFMA-bound and prefer 2 waves
     // without register spills (measured on the Netflix-shape workload, tools/kbench.py).
-    blk.min_waves = e->min_waves > 0 ? e->min_waves : (nnz_padded < (int64_t)tasks.size() * 1024 ? 3 : 2);
+    blk.min_waves = e->min_waves > 0 ? e->min_waves : 2;   // 2 waves/SIMD measured faster on both sides (tools/kbench.py)
     auto up = [&](void** dst, const void* src, size_t bytes) -> int {
         if (bytes == 0) return ALS_OK;
         hipError_t st = hipMalloc(dst, bytes);

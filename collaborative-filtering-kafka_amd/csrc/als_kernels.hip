@@ -271,22 +271,281 @@ struct MfmaAcc {
 template <int C>
 __host__ __device__ constexpr int tile_index(int b1, int b2) { return b1 * C - (b1 * (b1 - 1)) / 2 + (b2 - b1); }
 
+// ---------------------------------------------------------------------------------------------------
+// Cross-lane moves on the 4 x 16 lane grid (row g = lane >> 4, column c = lane & 15), VALU-only (no LDS)
+// ---------------------------------------------------------------------------------------------------
+// value of lane (g, L) at every lane of row g (DPP row_newbcast)
+template <int L>
+__device__ __forceinline__ float row_lane_bcast(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + L, 0xf, 0xf, false));
+}
+// value of lane (G, c) at every lane (g, c): v_permlane16_swap picks the even/odd row of each row pair,
+// v_permlane32_swap the low/high pair
+template <int G>
+__device__ __forceinline__ float col_bcast(float v) {
+    const int x = __float_as_int(v);
+    const auto s16 = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    const int y = (G & 1) ? (int)s16[1] : (int)s16[0];
+    const auto s32 = __builtin_amdgcn_permlane32_swap(y, y, false, false);
+    return __int_as_float((G & 2) ? (int)s32[1] : (int)s32[0]);
+}
+// sum over the 4 rows at each column, result in every row
+__device__ __forceinline__ float col_sum(float v) {
+    const int x = __float_as_int(v);
+    const auto s16 = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    const float y = __int_as_float((int)s16[0]) + __int_as_float((int)s16[1]);
+    const auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_int(y), __float_as_int(y), false, false);
+    return __int_as_float((int)s32[0]) + __int_as_float((int)s32[1]);
+}
+// inclusive row_shr scan: lane (g, 15) ends with the sum over row g
+__device__ __forceinline__ float row_sum_to_last(float v) {
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, true));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xf, 0xf, true));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xf, 0xf, true));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x118, 0xf, 0xf, true));
+    return v;
+}
+
+// Sweep operator (Goodnight) over all 16 pivots of one 16 x 16 tile in MFMA accumulator layout
+// (lane (g, c), register r holds a[4g + r][c]): in place a -> -a^{-1}. Step p:
+//   a[i][j] -= a[i][p] a[p][j] / d,  a[i][p] = a[i][p] / d,  a[p][j] = a[p][j] / d,  a[p][p] = -1 / d.
+// Column p reaches each row by DPP row_newbcast, row p each column by two permlane swaps. The pivot row /
+// column rules fold into the same four FMAs by offsetting a[p][p] by -1 in the broadcast operands:
+// a[i][p] + a[i][p] (d - 1)(-1/d) = a[i][p] / d. That FMA is accurate to a few ulp only while d <= 1,
+// which the caller guarantees by Jacobi-scaling the system to a unit diagonal (every later pivot is a
+// Schur-complement diagonal of a unit-diagonal SPD matrix, so it stays in (0, 1]).
+__device__ __forceinline__ void sweep_tile(f32x4& a, int lane) {
+    static_for<0, 16>([&](auto P_) {
+        constexpr int p = decltype(P_)::value;
+        constexpr int pg = p >> 2, pr = p & 3;
+        const float nrd = __builtin_amdgcn_rcpf(-bcast(a[pr], 16 * pg + p));   // -1 / d
+        const bool piv = opaque(lane) == 16 * pg + p;
+        a[pr] = piv ? a[pr] - 1.f : a[pr];
+        const float t = col_bcast<pg>(a[pr]) * nrd;                   // a[p][c] (d - 1 at c = p) * (-1/d)
+        f32x4 cp;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cp[r] = row_lane_bcast<p>(a[r]);   // a[4g + r][p] (d - 1 at row p)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a[r] += cp[r] * t;
+        a[pr] = piv ? nrd : a[pr];
+    });
+}
+
+// Block LDL^T solve on the Gram tiles left in the MFMA accumulators (no LDS copy of the matrix).
+// With C = KP/16 the accumulators hold G' = P G P^T (feature f = C*i + b at position 16*b + i) as upper
+// tiles T_IJ (I <= J) in accumulator layout; MFMA operands read straight from those registers because for
+// 16x16x4 the A/B slice s of lane (g, c) is "register s" of a tile read as X[4g+s][c] -- the k index runs
+// over the rows of the tile, which is exactly what T_PI^T V and A^{-1} T need. Per block column P:
+//   S = sweep(T_PP) = -T_PP^{-1};  V'_PJ = S T_PJ (= -T_PP^{-1} T_PJ);  T_IJ += T_PI^T V'_PJ (P < I <= J);
+//   forward  b_I += V'_PI^T b_P,  u_P = S b_P;  backward  x_P = -u_P + sum_{I>P} V'_PI x_I.
+// The explicit block inverses cost accuracy on ill-conditioned diagonal blocks (forward error grows with
+// cond(T_PP), not just cond(A)), so the solve ends with one step of iterative refinement against the
+// (scaled, regularised) Gram kept in registers: r = b - A x, x += solve(r). That brings the fp32 error
+// below the reference's own fp32 LU (tests/test_gpu_parity.py). Vectors are held "lane (g, j) = element j"
+// of each block; buf is KP floats of per-wave LDS.
+template <int C>
+__device__ __forceinline__ void solve_tiles(MfmaAcc<C>& acc, float* buf, const Task& tk, const SolveArgs& a,
+                                            int lane) {
+    constexpr int NT = MfmaAcc<C>::NT;
+    const int g = lane >> 4, j = lane & 15;
+    float* out = (float*)a.out + (a.row_offset + tk.row) * (int64_t)(16 * C);
+    if (tk.ndeg == 0) {   // cannot occur in the reference (entities exist only once rated); defined as 0
+        if (g == 0) {
+#pragma unroll
+            for (int b = 0; b < C; ++b) out[C * j + b] = 0.f;
+        }
+        return;
+    }
+    // A + lambda * (n * I) (fp32, MFeatureCalculator.java:91-95: A[f][f] + lambda*(float)n); padded features
+    // get an identity row (their Gram rows/columns are exactly zero: padded factor columns are zero).
+    // Then Jacobi scaling A' = D A D, b' = D b, x = D x' with D = diag(A)^{-1/2}: lane (g, j) of block b
+    // needs s for column j (scol) and for rows 4g..4g+3 (srow), exchanged through buf.
+    const float reg = a.lambda * (float)tk.ndeg;
+    const int jr = j & 3;
+    const bool diag_lane = opaque(j >> 2) == g;   // lane holds a diagonal entry, in register j & 3
+    float scol[C];
+    f32x4 srow[C];
+#pragma unroll
+    for (int b = 0; b < C; ++b) {
+        f32x4& t = acc.g[tile_index<C>(b, b)];
+        const bool real = C * j + b < a.k;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const bool diag = diag_lane && jr == r;
+            t[r] = diag ? (real ? t[r] + reg : 1.f) : t[r];
+        }
+        float dv = t[0];
+#pragma unroll
+        for (int r = 1; r < 4; ++r) dv = (jr == r) ? t[r] : dv;
+        if (diag_lane) buf[16 * b + j] = __builtin_amdgcn_rsqf(dv);
+    }
+    wave_sync();
+#pragma unroll
+    for (int b = 0; b < C; ++b) {
+        scol[b] = buf[16 * b + j];
+        srow[b] = *(const f32x4*)(buf + 16 * b + 4 * g);
+    }
+    wave_sync();
+    f32x4 A0[NT];        // the scaled system, kept for the refinement residual
+#pragma unroll
+    for (int I = 0; I < C; ++I)
+#pragma unroll
+        for (int J = I; J < C; ++J) {
+            f32x4& t = acc.g[tile_index<C>(I, J)];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t[r] *= srow[I][r] * scol[J];
+            A0[tile_index<C>(I, J)] = t;
+        }
+    float b0[C];
+#pragma unroll
+    for (int b = 0; b < C; ++b) b0[b] = col_sum(acc.rhs[b]) * scol[b];
+
+    // ---- factorisation (matrix part only) ----
+    static_for<0, C>([&](auto P_) {
+        constexpr int P = decltype(P_)::value;
+        f32x4& S = acc.g[tile_index<C>(P, P)];
+        sweep_tile(S, lane);
+        f32x4 V[C];
+        static_for<P + 1, C>([&](auto J_) {
+            constexpr int J = decltype(J_)::value;
+            const f32x4 T = acc.g[tile_index<C>(P, J)];
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) v = __builtin_amdgcn_mfma_f32_16x16x4f32(S[s], T[s], v, 0, 0, 0);
+            V[J] = v;
+        });
+        static_for<P + 1, C>([&](auto I_) {
+            constexpr int I = decltype(I_)::value;
+            const f32x4 TPI = acc.g[tile_index<C>(P, I)];
+            static_for<I, C>([&](auto J_) {
+                constexpr int J = decltype(J_)::value;
+                f32x4& T = acc.g[tile_index<C>(I, J)];
+#pragma unroll
+                for (int s = 0; s < 4; ++s) T = __builtin_amdgcn_mfma_f32_16x16x4f32(TPI[s], V[J][s], T, 0, 0, 0);
+            });
+        });
+        static_for<P + 1, C>([&](auto J_) {
+            constexpr int J = decltype(J_)::value;
+            acc.g[tile_index<C>(P, J)] = V[J];   // block row P now holds V'_PJ
+        });
+    });
+
+    // ---- x = A^{-1} rhs with the factorisation ----
+    auto solve_vec = [&](const float (&rhs)[C], float (&x)[C]) {
+        float bw[C], u[C];
+#pragma unroll
+        for (int b = 0; b < C; ++b) bw[b] = rhs[b];
+        static_for<0, C>([&](auto P_) {
+            constexpr int P = decltype(P_)::value;
+            const f32x4& S = acc.g[tile_index<C>(P, P)];
+            wave_sync();
+            if (g == 0) buf[j] = bw[P];           // b_P[4g + r] into every lane of row g
+            wave_sync();
+            const f32x4 bb = *(const f32x4*)(buf + 4 * g);
+            float su = 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) su += S[r] * bb[r];
+            u[P] = col_sum(su);
+            static_for<P + 1, C>([&](auto I_) {
+                constexpr int I = decltype(I_)::value;
+                const f32x4& V = acc.g[tile_index<C>(P, I)];
+                float sb = 0.f;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sb += V[r] * bb[r];
+                bw[I] += col_sum(sb);
+            });
+        });
+        static_for<0, C>([&](auto Q_) {
+            constexpr int P = C - 1 - decltype(Q_)::value;
+            if constexpr (P == C - 1) {
+                x[P] = -u[P];
+            } else {
+                f32x4 w = {0.f, 0.f, 0.f, 0.f};
+                static_for<P + 1, C>([&](auto I_) {
+                    constexpr int I = decltype(I_)::value;
+                    const f32x4& V = acc.g[tile_index<C>(P, I)];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) w[r] += V[r] * x[I];
+                });
+#pragma unroll
+                for (int r = 0; r < 4; ++r) w[r] = row_sum_to_last(w[r]);
+                wave_sync();
+                if (j == 15) *(f32x4*)(buf + 4 * g) = w;
+                wave_sync();
+                x[P] = buf[j] - u[P];
+            }
+        });
+    };
+    float x[C];
+    solve_vec(b0, x);
+
+    // ---- one refinement step: r = b - A x over the kept upper tiles (A_IJ and A_IJ^T), x += A^{-1} r ----
+    wave_sync();
+    if (g == 0) {
+#pragma unroll
+        for (int b = 0; b < C; ++b) buf[16 * b + j] = x[b];
+    }
+    wave_sync();
+    f32x4 xr[C];                                   // x_b[4g + q] in row g
+#pragma unroll
+    for (int b = 0; b < C; ++b) xr[b] = *(const f32x4*)(buf + 16 * b + 4 * g);
+    float res[C];
+    f32x4 w[C];
+#pragma unroll
+    for (int b = 0; b < C; ++b) {
+        res[b] = 0.f;
+        w[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int I = 0; I < C; ++I)
+#pragma unroll
+        for (int J = I; J < C; ++J) {
+            const f32x4& t = A0[tile_index<C>(I, J)];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) w[I][q] += t[q] * x[J];            // rows of block I
+            if (I != J) {
+                float s = 0.f;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) s += t[q] * xr[I][q];          // (A_IJ^T x_I) at column c
+                res[J] += s;
+            }
+        }
+#pragma unroll
+    for (int b = 0; b < C; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[b][q] = row_sum_to_last(w[b][q]);
+    wave_sync();
+    if (j == 15) {
+#pragma unroll
+        for (int b = 0; b < C; ++b) *(f32x4*)(buf + 16 * b + 4 * g) = w[b];
+    }
+    wave_sync();
+    float r[C];
+#pragma unroll
+    for (int b = 0; b < C; ++b) r[b] = b0[b] - buf[16 * b + j] - (C > 1 ? col_sum(res[b]) : 0.f);
+    float dx[C];
+    solve_vec(r, dx);
+    if (g == 0) {
+        using VT = typename VecC<C>::type;
+        VT o;
+#pragma unroll
+        for (int b = 0; b < C; ++b) o[b] = (C * j + b < a.k) ? (x[b] + dx[b]) * scol[b] : 0.f;
+        *(VT*)(out + C * j) = o;
+    }
+}
+
 template <int KP, int MINW>
 __global__ __launch_bounds__(256, MINW) void als_solve_mfma(SolveArgs a) {
     constexpr int C = KP / 16;
     using Acc = MfmaAcc<C>;
     using VT = typename VecC<C>::type;
-    using L = WaveLds<float, KP, Path::MFMA>;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ __attribute__((aligned(16))) float sbuf[WAVES][KP];
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tid = blockIdx.x * WAVES + wave;
     if (tid >= a.n_tasks) return;   // wave-uniform; no workgroup barriers are used below
     const Task tk = load_task(a.tasks + tid);
-    unsigned char* wl = smem + wave * L::BYTES;
-    float* G = (float*)wl;
-    float* rhs_l = (float*)(wl + L::RHS_OFF);
-    float* bc = (float*)(wl + L::BC_OFF);
+    float* buf = sbuf[wave];
 
     const int g = lane >> 4, j = lane & 15;
     Acc acc;
@@ -385,29 +644,7 @@ __global__ __launch_bounds__(256, MINW) void als_solve_mfma(SolveArgs a) {
         return;
     }
 
-    // Canonicalise into the packed lower triangle: tile (b1,b2) lane (g,j) reg r holds G[C*(4g+r)+b1][C*j+b2];
-    // every unordered pair {row, col} occurs exactly once over the b1 <= b2 tiles (both orders inside a
-    // diagonal tile, where only row >= col is stored).
-#pragma unroll
-    for (int b1 = 0; b1 < C; ++b1)
-#pragma unroll
-        for (int b2 = b1; b2 < C; ++b2)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float v = acc.g[tile_index<C>(b1, b2)][r];
-                const int row = C * (4 * g + r) + b1, col = C * j + b2;
-                if (row >= col) G[tri(row, 0) + col] = v;
-                else if (b1 != b2) G[tri(col, 0) + row] = v;
-            }
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-        float v = acc.rhs[c];
-        v += __shfl_xor(v, 16);
-        v += __shfl_xor(v, 32);
-        if (g == 0) rhs_l[C * j + c] = v;
-    }
-    wave_sync();
-    solve_store<float, KP>(G, rhs_l, bc, tk, a, lane);
+    solve_tiles<C>(acc, buf, tk, a, lane);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -553,14 +790,7 @@ hipError_t launch_solve_t(const SolveArgs& a, hipStream_t s) {
     constexpr int bytes = WAVES * WaveLds<T, KP, P>::BYTES;
     if constexpr (P == Path::MFMA) {
         static_assert(std::is_same<T, float>::value, "MFMA path is fp32");
-        static bool attr = false;
-        if (!attr) {
-            hipError_t e = hipFuncSetAttribute((const void*)als_solve_mfma<KP, MINW>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-            if (e != hipSuccess) return e;
-            attr = true;
-        }
-        als_solve_mfma<KP, MINW><<<blocks_for(a.n_tasks), 256, bytes, s>>>(a);
+        als_solve_mfma<KP, MINW><<<blocks_for(a.n_tasks), 256, 0, s>>>(a);
     } else {
         static bool attr = false;
         if (!attr) {

@@ -84,7 +84,11 @@ def _synthetic(cfk, oracle_mod, n_users=3000, n_movies=400, nnz=90_000, seed=11)
 
 @pytest.mark.parametrize("k", [1, 5, 10, 16, 17, 31, 32, 33, 48, 63, 64])
 def test_one_half_every_k_vs_oracle(cfk, oracle_mod, k):
-    """Both sides, f64 (VALU path) to 1e-9 and f32 (VALU k<32 / MFMA k>=32) to norm-rel 1e-4."""
+    """Both sides. f64 (VALU path) to 1e-7 max-rel. f32 (VALU k<32 / MFMA tile solve k>=32) against the exact
+    solution, held to the error envelope of the reference's OWN fp32 arithmetic on the same rows (the oracle's
+    f32 mode restates EJML's fp32 LU): per-row norm-relative error p99 <= 2x and max <= 3x the reference's,
+    with floors 2e-5 / 1e-4. The worst rows on both paths are users with one rating (A = y y^T + 0.05 I,
+    condition number ~ k/0.15), where the reference itself is off by up to ~1e-3 at k = 64."""
     ds, b = _synthetic(cfk, oracle_mod)
     rng = np.random.default_rng(k)
     for side, rows, opp in ((0, b.movie, b.user), (1, b.user, b.movie)):
@@ -94,8 +98,12 @@ def test_one_half_every_k_vs_oracle(cfk, oracle_mod, k):
         got64 = _one_half(cfk, side, blk, F, k, "f64", len(opp.ids))
         assert max_rel(got64, ref) <= 1e-7, (side, k)          # 10x inside the 1e-6 bar
         got32 = _one_half(cfk, side, blk, F.astype(np.float32), k, "f32", len(opp.ids))
-        rel = np.linalg.norm(got32 - ref, axis=1) / np.linalg.norm(ref, axis=1)
-        assert rel.max() <= 1e-4, (side, k, rel.max())
+        ref32 = oracle_mod.update_side(rows, F.astype(np.float32), LAM, "f32")
+        norm = np.linalg.norm(ref, axis=1)
+        rel = np.linalg.norm(got32 - ref, axis=1) / norm
+        rel_ref = np.linalg.norm(ref32 - ref, axis=1) / norm
+        assert np.percentile(rel, 99) <= max(2 * np.percentile(rel_ref, 99), 2e-5), (side, k)
+        assert rel.max() <= max(3 * rel_ref.max(), 1e-4), (side, k, rel.max(), rel_ref.max())
 
 
 @pytest.mark.parametrize("chunk", ["4", "64", "256"])
