@@ -194,7 +194,7 @@ def main():
             cpu = cpu_baseline(ds, args.k, args.lam, args.cpu_seconds, min(16, os.cpu_count() or 1))
         value = nnz * K / elapsed
         line = {
-            "metric": "ALS ratings/sec per full iteration, k=64 Netflix-shape",
+            "metric": "ALS ratings/sec per full iteration, k=64 Netflix-shape, 1/2/4/8 MI355X",
             "value": value, "unit": "ratings/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
             "ms_per_step": elapsed / K * 1000.0, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded Netflix-shape generator)",

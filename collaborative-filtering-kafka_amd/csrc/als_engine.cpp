@@ -135,8 +135,9 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
         return fail(ALS_ERR_INVALID_ARGUMENT, "precision must be ALS_F32 or ALS_F64");
     if (num_features < 1) return fail(ALS_ERR_INVALID_ARGUMENT, "num_features must be >= 1, got %d", num_features);
     int kp = num_features <= 16 ? 16 : num_features <= 32 ? 32 : num_features <= 64 ? 64 : 128;
-    if (num_features > 64)
-        return fail(ALS_ERR_UNSUPPORTED, "num_features=%d: this build supports 1..64", num_features);
+    if (num_features > 128 || (precision == ALS_F64 && num_features > 64))
+        return fail(ALS_ERR_UNSUPPORTED, "num_features=%d: this build supports 1..128 (f32) / 1..64 (f64)",
+                    num_features);
     // MFMA Gram only where the accumulation is a real dense contraction (k >= 32, north star); fp64 and
     // small k use the LDS-staged VALU Gram.
     Path path = (precision == ALS_F32 && num_features >= 32) ? Path::MFMA : Path::VALU;

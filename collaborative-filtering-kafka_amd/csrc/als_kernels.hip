@@ -34,6 +34,7 @@ constexpr int RSTAGE = 64;     // VALU path: rows staged per LDS block
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 
 template <class T> struct Vec16;
@@ -43,6 +44,7 @@ template <> struct Vec16<double> { typedef f64x2 type; static constexpr int N = 
 template <int C> struct VecC;
 template <> struct VecC<2> { typedef f32x2 type; };
 template <> struct VecC<4> { typedef f32x4 type; };
+template <> struct VecC<8> { typedef f32x8 type; };
 
 // Same-wave LDS hand-off: the hardware keeps one wave's DS operations in order; this only stops the
 // compiler from moving LDS accesses across the point.
@@ -343,10 +345,44 @@ __device__ __forceinline__ void sweep_tile(f32x4& a, int lane) {
 // (scaled, regularised) Gram kept in registers: r = b - A x, x += solve(r). That brings the fp32 error
 // below the reference's own fp32 LU (tests/test_gpu_parity.py). Vectors are held "lane (g, j) = element j"
 // of each block; buf is KP floats of per-wave LDS.
+// Tile storage of the solve. Up to KP = 64 the tiles stay in the MFMA accumulator registers (RegTiles);
+// at KP = 128 (36 tiles = 144 registers per copy; the solve's VALU work needs them in the 256 architected
+// VGPRs) the working tiles and the kept copy live in per-wave LDS ([tile][reg][lane]: conflict-free b32
+// accesses) and are loaded a tile at a time (LdsTiles).
 template <int C>
-__device__ __forceinline__ void solve_tiles(MfmaAcc<C>& acc, float* buf, const Task& tk, const SolveArgs& a,
-                                            int lane) {
-    constexpr int NT = MfmaAcc<C>::NT;
+struct RegTiles {
+    f32x4* t;
+    __device__ __forceinline__ f32x4 get(int i) const { return t[i]; }
+    __device__ __forceinline__ void put(int i, const f32x4& v) { t[i] = v; }
+};
+template <int C>
+struct RegStore {
+    f32x4 t[MfmaAcc<C>::NT];
+    __device__ __forceinline__ f32x4 get(int i) const { return t[i]; }
+    __device__ __forceinline__ void put(int i, const f32x4& v) { t[i] = v; }
+};
+struct LdsTiles {
+    float* p;   // per-wave base + lane
+    __device__ __forceinline__ f32x4 get(int i) const {
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = p[(i * 4 + r) * 64];
+        return v;
+    }
+    __device__ __forceinline__ void put(int i, const f32x4& v) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) p[(i * 4 + r) * 64] = v[r];
+    }
+};
+template <int C>
+constexpr bool tiles_in_lds() { return C > 4; }
+template <int C>
+constexpr int tile_lds_floats() { return tiles_in_lds<C>() ? MfmaAcc<C>::NT * 4 * 64 : 0; }
+
+// T: working tiles (RegTiles / LdsTiles), A0: kept copy of the scaled system (RegStore / LdsTiles).
+template <int C, class TT, class KT>
+__device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc)[C], float* buf, const Task& tk,
+                                            const SolveArgs& a, int lane) {
     const int g = lane >> 4, j = lane & 15;
     float* out = (float*)a.out + (a.row_offset + tk.row) * (int64_t)(16 * C);
     if (tk.ndeg == 0) {   // cannot occur in the reference (entities exist only once rated); defined as 0
@@ -367,13 +403,14 @@ __device__ __forceinline__ void solve_tiles(MfmaAcc<C>& acc, float* buf, const T
     f32x4 srow[C];
 #pragma unroll
     for (int b = 0; b < C; ++b) {
-        f32x4& t = acc.g[tile_index<C>(b, b)];
+        f32x4 t = T.get(tile_index<C>(b, b));
         const bool real = C * j + b < a.k;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const bool diag = diag_lane && jr == r;
             t[r] = diag ? (real ? t[r] + reg : 1.f) : t[r];
         }
+        T.put(tile_index<C>(b, b), t);
         float dv = t[0];
 #pragma unroll
         for (int r = 1; r < 4; ++r) dv = (jr == r) ? t[r] : dv;
@@ -386,47 +423,44 @@ __device__ __forceinline__ void solve_tiles(MfmaAcc<C>& acc, float* buf, const T
         srow[b] = *(const f32x4*)(buf + 16 * b + 4 * g);
     }
     wave_sync();
-    f32x4 A0[NT];        // the scaled system, kept for the refinement residual
 #pragma unroll
     for (int I = 0; I < C; ++I)
 #pragma unroll
         for (int J = I; J < C; ++J) {
-            f32x4& t = acc.g[tile_index<C>(I, J)];
+            f32x4 t = T.get(tile_index<C>(I, J));
 #pragma unroll
             for (int r = 0; r < 4; ++r) t[r] *= srow[I][r] * scol[J];
-            A0[tile_index<C>(I, J)] = t;
+            T.put(tile_index<C>(I, J), t);
+            A0.put(tile_index<C>(I, J), t);
         }
     float b0[C];
 #pragma unroll
-    for (int b = 0; b < C; ++b) b0[b] = col_sum(acc.rhs[b]) * scol[b];
+    for (int b = 0; b < C; ++b) b0[b] = col_sum(rhs_acc[b]) * scol[b];
 
     // ---- factorisation (matrix part only) ----
     static_for<0, C>([&](auto P_) {
         constexpr int P = decltype(P_)::value;
-        f32x4& S = acc.g[tile_index<C>(P, P)];
+        f32x4 S = T.get(tile_index<C>(P, P));
         sweep_tile(S, lane);
-        f32x4 V[C];
-        static_for<P + 1, C>([&](auto J_) {
-            constexpr int J = decltype(J_)::value;
-            const f32x4 T = acc.g[tile_index<C>(P, J)];
+        T.put(tile_index<C>(P, P), S);
+        // Block columns J in DESCENDING order: V'_PJ only updates T_IJ (P < I <= J) from the still-unreplaced
+        // T_PI (I <= J), so block row P can take V'_PJ right away and one V is live at a time. Every T_IJ
+        // receives the same single update per P as in any order: bitwise equal.
+        static_for<0, C - 1 - P>([&](auto Q_) {
+            constexpr int J = C - 1 - decltype(Q_)::value;
+            const f32x4 TPJ = T.get(tile_index<C>(P, J));
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int s = 0; s < 4; ++s) v = __builtin_amdgcn_mfma_f32_16x16x4f32(S[s], T[s], v, 0, 0, 0);
-            V[J] = v;
-        });
-        static_for<P + 1, C>([&](auto I_) {
-            constexpr int I = decltype(I_)::value;
-            const f32x4 TPI = acc.g[tile_index<C>(P, I)];
-            static_for<I, C>([&](auto J_) {
-                constexpr int J = decltype(J_)::value;
-                f32x4& T = acc.g[tile_index<C>(I, J)];
+            for (int s = 0; s < 4; ++s) v = __builtin_amdgcn_mfma_f32_16x16x4f32(S[s], TPJ[s], v, 0, 0, 0);
+            static_for<P + 1, J + 1>([&](auto I_) {
+                constexpr int I = decltype(I_)::value;
+                const f32x4 TPI = T.get(tile_index<C>(P, I));
+                f32x4 D = T.get(tile_index<C>(I, J));
 #pragma unroll
-                for (int s = 0; s < 4; ++s) T = __builtin_amdgcn_mfma_f32_16x16x4f32(TPI[s], V[J][s], T, 0, 0, 0);
+                for (int s = 0; s < 4; ++s) D = __builtin_amdgcn_mfma_f32_16x16x4f32(TPI[s], v[s], D, 0, 0, 0);
+                T.put(tile_index<C>(I, J), D);
             });
-        });
-        static_for<P + 1, C>([&](auto J_) {
-            constexpr int J = decltype(J_)::value;
-            acc.g[tile_index<C>(P, J)] = V[J];   // block row P now holds V'_PJ
+            T.put(tile_index<C>(P, J), v);   // block row P now holds V'_PJ
         });
     });
 
@@ -437,7 +471,7 @@ __device__ __forceinline__ void solve_tiles(MfmaAcc<C>& acc, float* buf, const T
         for (int b = 0; b < C; ++b) bw[b] = rhs[b];
         static_for<0, C>([&](auto P_) {
             constexpr int P = decltype(P_)::value;
-            const f32x4& S = acc.g[tile_index<C>(P, P)];
+            const f32x4 S = T.get(tile_index<C>(P, P));
             wave_sync();
             if (g == 0) buf[j] = bw[P];           // b_P[4g + r] into every lane of row g
             wave_sync();
@@ -448,7 +482,7 @@ __device__ __forceinline__ void solve_tiles(MfmaAcc<C>& acc, float* buf, const T
             u[P] = col_sum(su);
             static_for<P + 1, C>([&](auto I_) {
                 constexpr int I = decltype(I_)::value;
-                const f32x4& V = acc.g[tile_index<C>(P, I)];
+                const f32x4 V = T.get(tile_index<C>(P, I));
                 float sb = 0.f;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) sb += V[r] * bb[r];
@@ -463,7 +497,7 @@ __device__ __forceinline__ void solve_tiles(MfmaAcc<C>& acc, float* buf, const T
                 f32x4 w = {0.f, 0.f, 0.f, 0.f};
                 static_for<P + 1, C>([&](auto I_) {
                     constexpr int I = decltype(I_)::value;
-                    const f32x4& V = acc.g[tile_index<C>(P, I)];
+                    const f32x4 V = T.get(tile_index<C>(P, I));
 #pragma unroll
                     for (int r = 0; r < 4; ++r) w[r] += V[r] * x[I];
                 });
@@ -500,7 +534,7 @@ __device__ __forceinline__ void solve_tiles(MfmaAcc<C>& acc, float* buf, const T
     for (int I = 0; I < C; ++I)
 #pragma unroll
         for (int J = I; J < C; ++J) {
-            const f32x4& t = A0[tile_index<C>(I, J)];
+            const f32x4 t = A0.get(tile_index<C>(I, J));
 #pragma unroll
             for (int q = 0; q < 4; ++q) w[I][q] += t[q] * x[J];            // rows of block I
             if (I != J) {
@@ -534,15 +568,23 @@ __device__ __forceinline__ void solve_tiles(MfmaAcc<C>& acc, float* buf, const T
     }
 }
 
+// Waves (tasks) per workgroup of the MFMA kernel: 4, or 2 at KP = 128, whose 72 KB of per-wave LDS tiles
+// allow two 2-wave workgroups per CU (one wave per SIMD, which its register use allows anyway).
+template <int KP>
+constexpr int mfma_waves() { return WAVES; }
+
 template <int KP, int MINW>
-__global__ __launch_bounds__(256, MINW) void als_solve_mfma(SolveArgs a) {
+__global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(SolveArgs a) {
     constexpr int C = KP / 16;
+    constexpr int NW = mfma_waves<KP>();
     using Acc = MfmaAcc<C>;
     using VT = typename VecC<C>::type;
-    __shared__ __attribute__((aligned(16))) float sbuf[WAVES][KP];
+    __shared__ __attribute__((aligned(16))) float sbuf[NW][KP];
+    constexpr int TL = tile_lds_floats<C>();
+    __shared__ __attribute__((aligned(16))) float tiles_lds[NW][TL > 0 ? TL : 1];
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tid = blockIdx.x * WAVES + wave;
+    const int tid = blockIdx.x * NW + wave;
     if (tid >= a.n_tasks) return;   // wave-uniform; no workgroup barriers are used below
     const Task tk = load_task(a.tasks + tid);
     float* buf = sbuf[wave];
@@ -605,7 +647,55 @@ __global__ __launch_bounds__(256, MINW) void als_solve_mfma(SolveArgs a) {
 #pragma unroll
             for (int c = 0; c < C; ++c) acc.rhs[c] += r * y[c];
         };
-        if (nblk > 0) {
+        if constexpr (C > 4) {
+            // KP = 128: 288 MFMAs per block, so half a block of prefetch (4 gathered rows per lane in
+            // flight) covers the gather latency and halves the staging registers (the 36 accumulator
+            // tiles already take 144). Stage = 4 sub-steps = one 16-B index/rating vector per lane.
+            constexpr int H = B / 2;
+            auto gather_half = [&](const Idx& x, auto h_, VT (&y)[H]) {
+                constexpr int h = decltype(h_)::value;
+#pragma unroll
+                for (int t = 0; t < H; ++t)
+                    y[t] = *(const VT*)(obase + (uint32_t)x.i[h][t] * (uint32_t)(KP * sizeof(float)));
+            };
+            using H0 = std::integral_constant<int, 0>;
+            using H1 = std::integral_constant<int, 1>;
+            if (nblk > 0) {
+                Idx x_c, x_n;
+                VT y_c[H], y_n[H];
+                load_idx(0, x_c);
+                load_idx(nblk > 1 ? 1 : 0, x_n);
+                gather_half(x_c, H0{}, y_c);
+                for (int b = 0; b + 1 < nblk; ++b) {
+                    gather_half(x_c, H1{}, y_n);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int t = 0; t < H; ++t) mfma_step(y_c[t], x_c.r[0][t]);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int t = 0; t < H; ++t) y_c[t] = y_n[t];
+                    Idx x_nn;
+                    load_idx(b + 2 < nblk ? b + 2 : nblk - 1, x_nn);   // clamped: always a valid address
+                    gather_half(x_n, H0{}, y_n);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int t = 0; t < H; ++t) mfma_step(y_c[t], x_c.r[1][t]);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int t = 0; t < H; ++t) y_c[t] = y_n[t];
+                    x_c = x_n;
+                    x_n = x_nn;
+                }
+                const int last = n - (nblk - 1) * B;
+                gather_half(x_c, H1{}, y_n);
+#pragma unroll
+                for (int t = 0; t < H; ++t)
+                    if (t < last) mfma_step(y_c[t], x_c.r[0][t]);     // wave-uniform
+#pragma unroll
+                for (int t = 0; t < H; ++t)
+                    if (H + t < last) mfma_step(y_n[t], x_c.r[1][t]);
+            }
+        } else if (nblk > 0) {
             Idx x_c, x_n;
             VT y_c[B], y_n[B];
             load_idx(0, x_c);
@@ -644,7 +734,17 @@ __global__ __launch_bounds__(256, MINW) void als_solve_mfma(SolveArgs a) {
         return;
     }
 
-    solve_tiles<C>(acc, buf, tk, a, lane);
+    if constexpr (tiles_in_lds<C>()) {
+        LdsTiles T{tiles_lds[wave] + lane};
+        RegStore<C> A0;
+#pragma unroll
+        for (int p = 0; p < Acc::NT; ++p) T.put(p, acc.g[p]);
+        solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
+    } else {
+        RegTiles<C> T{acc.g};
+        RegStore<C> A0;
+        solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -790,7 +890,8 @@ hipError_t launch_solve_t(const SolveArgs& a, hipStream_t s) {
     constexpr int bytes = WAVES * WaveLds<T, KP, P>::BYTES;
     if constexpr (P == Path::MFMA) {
         static_assert(std::is_same<T, float>::value, "MFMA path is fp32");
-        als_solve_mfma<KP, MINW><<<blocks_for(a.n_tasks), 256, 0, s>>>(a);
+        constexpr int nw = mfma_waves<KP>();
+        als_solve_mfma<KP, MINW><<<(a.n_tasks + nw - 1) / nw, 64 * nw, 0, s>>>(a);
     } else {
         static bool attr = false;
         if (!attr) {
@@ -815,7 +916,7 @@ hipError_t launch_sq_t(const SqErrArgs& a, hipStream_t s) {
 
 bool variant_available(int precision, int kp, Path path) {
     if (precision == 0) {
-        if (path == Path::MFMA) return kp == 32 || kp == 64;
+        if (path == Path::MFMA) return kp == 32 || kp == 64 || kp == 128;
         return kp == 16 || kp == 32 || kp == 64;
     }
     return path == Path::VALU && (kp == 16 || kp == 32 || kp == 64);
@@ -835,6 +936,7 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
             if (kp == 32) return launch_solve_t<float, 32, Path::MFMA, 2>(a, s);
             if (kp == 64 && min_waves >= 3) return launch_solve_t<float, 64, Path::MFMA, 3>(a, s);
             if (kp == 64) return launch_solve_t<float, 64, Path::MFMA, 2>(a, s);
+            if (kp == 128) return launch_solve_t<float, 128, Path::MFMA, 1>(a, s);
         } else {
             if (kp == 16) return launch_solve_t<float, 16, Path::VALU>(a, s);
             if (kp == 32) return launch_solve_t<float, 32, Path::VALU>(a, s);
@@ -853,6 +955,7 @@ hipError_t launch_sq_error(int precision, int kp, const SqErrArgs& a, hipStream_
         if (kp == 16) return launch_sq_t<float, 16>(a, s);
         if (kp == 32) return launch_sq_t<float, 32>(a, s);
         if (kp == 64) return launch_sq_t<float, 64>(a, s);
+        if (kp == 128) return launch_sq_t<float, 128>(a, s);
     } else {
         if (kp == 16) return launch_sq_t<double, 16>(a, s);
         if (kp == 32) return launch_sq_t<double, 32>(a, s);

@@ -145,7 +145,9 @@ def test_error_behaviour(cfk, tmp_path):
     with pytest.raises(ALSError):
         cfk.ALSEngine(0, "f32")
     with pytest.raises(ALSError, match="ALS_ERR_UNSUPPORTED"):
-        cfk.ALSEngine(100, "f32")
+        cfk.ALSEngine(129, "f32")          # f32: 1..128
+    with pytest.raises(ALSError, match="ALS_ERR_UNSUPPORTED"):
+        cfk.ALSEngine(100, "f64")          # f64 parity mode: 1..64
 
 
 def test_cli_arguments_missing_message():
