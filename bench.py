@@ -182,7 +182,7 @@ def main():
         roofline = {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
-            "kernel": "als_solve_mfma<64> (fused gather + MFMA Gram + in-wave Cholesky), main launch of each half",
+            "kernel": "als_solve_mfma<64,2,split> (fused gather + split-bf16 MFMA Gram + in-wave tile LDL^T solve), main launch of each half",
             "algorithmic_bytes_per_launch": (b_movie + b_user) / 2,
             "avg_launch_ms": {"movie": gm / max(cm, 1), "user": gu / max(cu, 1)},
             "reduce_launch_ms": {"movie": rm / max(cm, 1), "user": ru / max(cu, 1)},

@@ -139,8 +139,12 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
         return fail(ALS_ERR_UNSUPPORTED, "num_features=%d: this build supports 1..128 (f32) / 1..64 (f64)",
                     num_features);
     // MFMA Gram only where the accumulation is a real dense contraction (k >= 32, north star); fp64 and
-    // small k use the LDS-staged VALU Gram.
-    Path path = (precision == ALS_F32 && num_features >= 32) ? Path::MFMA : Path::VALU;
+    // small k use the LDS-staged VALU Gram. fp32 Gram products via the exact three-term bf16 split (Path::MFMA_SPLIT) by default;
+    // ALS_GRAM=f32 selects the v_mfma_f32_16x16x4_f32 path (same accumulator layout, 2.3x the Gram time).
+    Path path = (precision == ALS_F32 && num_features >= 32) ? Path::MFMA_SPLIT : Path::VALU;
+    if (path == Path::MFMA_SPLIT)
+        if (const char* env = getenv("ALS_GRAM"))
+            if (!strcmp(env, "f32")) path = Path::MFMA;
     if (const char* env = getenv("ALS_FORCE_VALU"))
         if (env[0] == '1') path = Path::VALU;
     if (!cfk::variant_available(precision, kp, path))

@@ -66,7 +66,10 @@ struct SqErrArgs {
     int32_t sentinel;
 };
 
-enum class Path : int { VALU = 0, MFMA = 1 };
+// Gram paths: VALU (LDS-staged, fp32 k < 32 and all fp64), MFMA (v_mfma_f32_16x16x4_f32, exact f32
+// products), MFMA_SPLIT (fp32 operands split exactly into three bf16 terms, six v_mfma_f32_16x16x32_bf16
+// partial products per tile, fp32 accumulation: fp32-accurate products at 16x the f32 MFMA rate).
+enum class Path : int { VALU = 0, MFMA = 1, MFMA_SPLIT = 2 };
 
 // Launch helpers (defined in als_kernels.hip). Return hipSuccess or the launch error.
 // min_waves: occupancy target (waves per SIMD) of the MFMA variant (__launch_bounds__ second argument).

@@ -37,6 +37,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
 template <class T> struct Vec16;
 template <> struct Vec16<float> { typedef f32x4 type; static constexpr int N = 4; };
 template <> struct Vec16<double> { typedef f64x2 type; static constexpr int N = 2; };
@@ -262,6 +266,23 @@ __device__ __forceinline__ void solve_store(T* P, const T* rhs_l, T* bc, const T
 // ---------------------------------------------------------------------------------------------------
 // MFMA Gram path (fp32, KP = 16*C with C in {2, 4})
 // ---------------------------------------------------------------------------------------------------
+// Exact three-term bf16 split of two fp32 values, packed as bf16 pairs (element 0 = x0 in the low half):
+// x = h + m + l with h = bf16_rn(x), m = bf16_rn(x - h), l = bf16_rn(x - h - m). Each residual is exact in
+// fp32 and |m| <= 2^-9 |x|, |l| <= 2^-18 |x|, so the dropped partial products m*l, l*m, l*l of x*y are
+// below 2^-26 |x y| -- under the fp32 rounding of the product itself -- and every bf16 x bf16 partial
+// product is exact in the fp32 MFMA accumulation. 11 VALU instructions per pair.
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2));
+}
+__device__ __forceinline__ void split3(float x0, float x1, unsigned& h, unsigned& m, unsigned& l) {
+    h = pk_bf16(x0, x1);
+    const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xffff0000u);
+    m = pk_bf16(r0, r1);
+    const float s0 = r0 - __uint_as_float(m << 16), s1 = r1 - __uint_as_float(m & 0xffff0000u);
+    l = pk_bf16(s0, s1);
+}
+__device__ __forceinline__ bf16x8 as_bf16x8(const u32x4& v) { return __builtin_bit_cast(bf16x8, v); }
+
 template <int C>
 struct MfmaAcc {
     static constexpr int NT = C * (C + 1) / 2;     // upper-triangular tiles (b1 <= b2)
@@ -573,7 +594,7 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 template <int KP>
 constexpr int mfma_waves() { return WAVES; }
 
-template <int KP, int MINW>
+template <int KP, int MINW, bool SPLIT>
 __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(SolveArgs a) {
     constexpr int C = KP / 16;
     constexpr int NW = mfma_waves<KP>();
@@ -647,7 +668,64 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
 #pragma unroll
             for (int c = 0; c < C; ++c) acc.rhs[c] += r * y[c];
         };
-        if constexpr (C > 4) {
+        if constexpr (SPLIT) {
+            // Split-bf16 Gram: one v_mfma_f32_16x16x32_bf16 consumes a whole 32-entry block. Lane (g, j)
+            // holds A[i = j][k = 8g + t] = y_t[C*j + b] (its own gathered piece, component b, entry t of its
+            // group): with the interleaved feature order (f = C*i + b) the operands need no lane movement,
+            // and the accumulators come out in exactly the layout of the f32 path (tile (b1, b2) holds
+            // G[C*i + b1][C*j' + b2]), so the solve, the partial slots and the REDUCE pass are shared.
+            // Padding entries gather the sentinel zero row with rating 0, so the last block needs no mask.
+            auto split_step = [&](const VT (&y)[B], const Idx& x) {
+                u32x4 H[C], M[C], L[C];
+#pragma unroll
+                for (int b = 0; b < C; ++b)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        unsigned h, m, l;
+                        split3(y[2 * q][b], y[2 * q + 1][b], h, m, l);
+                        H[b][q] = h;
+                        M[b][q] = m;
+                        L[b][q] = l;
+                    }
+#pragma unroll
+                for (int b1 = 0; b1 < C; ++b1)
+#pragma unroll
+                    for (int b2 = b1; b2 < C; ++b2) {
+                        f32x4 t = acc.g[tile_index<C>(b1, b2)];
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(M[b1]), as_bf16x8(M[b2]), t, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(H[b1]), as_bf16x8(L[b2]), t, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(L[b1]), as_bf16x8(H[b2]), t, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(H[b1]), as_bf16x8(M[b2]), t, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(M[b1]), as_bf16x8(H[b2]), t, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(H[b1]), as_bf16x8(H[b2]), t, 0, 0, 0);
+                        acc.g[tile_index<C>(b1, b2)] = t;
+                    }
+#pragma unroll
+                for (int t = 0; t < B; ++t)
+#pragma unroll
+                    for (int c = 0; c < C; ++c) acc.rhs[c] += x.r[t >> 2][t & 3] * y[t][c];
+            };
+            if (nblk > 0) {
+                Idx x_c, x_n;
+                VT y_c[B], y_n[B];
+                load_idx(0, x_c);
+                load_idx(nblk > 1 ? 1 : 0, x_n);
+                gather(x_c, y_c);
+                for (int b = 0; b + 1 < nblk; ++b) {
+                    Idx x_nn;
+                    load_idx(b + 2 < nblk ? b + 2 : nblk - 1, x_nn);   // clamped: always a valid address
+                    gather(x_n, y_n);
+                    __builtin_amdgcn_sched_barrier(0);
+                    split_step(y_c, x_c);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int t = 0; t < B; ++t) y_c[t] = y_n[t];
+                    x_c = x_n;
+                    x_n = x_nn;
+                }
+                split_step(y_c, x_c);
+            }
+        } else if constexpr (C > 4) {
             // KP = 128: 288 MFMAs per block, so half a block of prefetch (4 gathered rows per lane in
             // flight) covers the gather latency and halves the staging registers (the 36 accumulator
             // tiles already take 144). Stage = 4 sub-steps = one 16-B index/rating vector per lane.
@@ -888,10 +966,10 @@ template <class T, int KP, Path P, int MINW = 1>
 hipError_t launch_solve_t(const SolveArgs& a, hipStream_t s) {
     if (a.n_tasks <= 0) return hipSuccess;
     constexpr int bytes = WAVES * WaveLds<T, KP, P>::BYTES;
-    if constexpr (P == Path::MFMA) {
-        static_assert(std::is_same<T, float>::value, "MFMA path is fp32");
+    if constexpr (P == Path::MFMA || P == Path::MFMA_SPLIT) {
+        static_assert(std::is_same<T, float>::value, "MFMA paths are fp32");
         constexpr int nw = mfma_waves<KP>();
-        als_solve_mfma<KP, MINW><<<(a.n_tasks + nw - 1) / nw, 64 * nw, 0, s>>>(a);
+        als_solve_mfma<KP, MINW, P == Path::MFMA_SPLIT><<<(a.n_tasks + nw - 1) / nw, 64 * nw, 0, s>>>(a);
     } else {
         static bool attr = false;
         if (!attr) {
@@ -916,14 +994,14 @@ hipError_t launch_sq_t(const SqErrArgs& a, hipStream_t s) {
 
 bool variant_available(int precision, int kp, Path path) {
     if (precision == 0) {
-        if (path == Path::MFMA) return kp == 32 || kp == 64 || kp == 128;
+        if (path == Path::MFMA || path == Path::MFMA_SPLIT) return kp == 32 || kp == 64 || kp == 128;
         return kp == 16 || kp == 32 || kp == 64;
     }
     return path == Path::VALU && (kp == 16 || kp == 32 || kp == 64);
 }
 
 int partial_words_per_lane(int precision, int kp, Path path) {
-    if (path == Path::MFMA) {
+    if (path == Path::MFMA || path == Path::MFMA_SPLIT) {
         const int c = kp / 16;
         return (c * (c + 1) / 2) * 4 + c;
     }
@@ -937,6 +1015,10 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
             if (kp == 64 && min_waves >= 3) return launch_solve_t<float, 64, Path::MFMA, 3>(a, s);
             if (kp == 64) return launch_solve_t<float, 64, Path::MFMA, 2>(a, s);
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA, 1>(a, s);
+        } else if (path == Path::MFMA_SPLIT) {
+            if (kp == 32) return launch_solve_t<float, 32, Path::MFMA_SPLIT, 2>(a, s);
+            if (kp == 64) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2>(a, s);
+            if (kp == 128) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1>(a, s);
         } else {
             if (kp == 16) return launch_solve_t<float, 16, Path::VALU>(a, s);
             if (kp == 32) return launch_solve_t<float, 32, Path::VALU>(a, s);
