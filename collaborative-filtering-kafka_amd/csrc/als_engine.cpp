@@ -80,6 +80,7 @@ struct als_engine {
     void* d_partials = nullptr;
     size_t partial_bytes = 0;
     int min_waves = 0;              // ALS_MFMA_WAVES override of the per-block occupancy choice (0 = auto)
+    int32_t debug_flags = 0;        // ALS_DEBUG_SKIP_SOLVE=1 -> cfk::SOLVE_FLAG_SKIP_SOLVE (tools/kbench.py only)
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     std::vector<TimingRec> pending;
@@ -160,6 +161,10 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
     e->precision = precision;
     e->path = path;
     if (const char* env = getenv("ALS_MFMA_WAVES")) e->min_waves = std::max(0, atoi(env));
+    if (const char* env = getenv("ALS_DEBUG_SKIP_SOLVE"))
+        if (env[0] == '1') e->debug_flags |= cfk::SOLVE_FLAG_SKIP_SOLVE;
+    if (const char* env = getenv("ALS_DEBUG_SKIP_REFINE"))
+        if (env[0] == '1') e->debug_flags |= cfk::SOLVE_FLAG_SKIP_REFINE;
     hipError_t st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (st != hipSuccess) {
         delete e;
@@ -308,7 +313,9 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
     // Many short tasks (user side: ~200 ratings, one 64x64 solve each) are bound by the solve's VALU work
     // and gain from a third wave per SIMD; long chunks (movie side) are MFMA-bound and prefer 2 waves
     // without register spills (measured on the Netflix-shape workload, tools/kbench.py).
-    blk.min_waves = e->min_waves > 0 ? e->min_waves : 2;   // 2 waves/SIMD measured faster on both sides (tools/kbench.py)
+    // split-bf16 Gram: 3 waves/SIMD (no gather prefetch) measured 2-3% faster than 2 waves with ping-pong
+    // prefetch on both sides of the Netflix-shape workload (tools/kbench.py); the f32 MFMA path prefers 2.
+    blk.min_waves = e->min_waves > 0 ? e->min_waves : (e->path == Path::MFMA_SPLIT ? 3 : 2);
     auto up = [&](void** dst, const void* src, size_t bytes) -> int {
         if (bytes == 0) return ALS_OK;
         hipError_t st = hipMalloc(dst, bytes);
@@ -444,6 +451,7 @@ int als_solve_half(als_engine* e, int side, float lambda) {
     a.partials = e->d_partials;
     a.lambda = lambda;
     a.sentinel = (int32_t)b.n_opp_rows;
+    a.flags = e->path == Path::VALU ? 0 : e->debug_flags;
     TimingRec rec{side, {nullptr, nullptr, nullptr}};
     if (e->timing) {
         for (auto& ev : rec.ev) {

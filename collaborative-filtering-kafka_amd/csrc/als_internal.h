@@ -52,7 +52,12 @@ struct SolveArgs {
     void* partials;         // partial-slot workspace
     float lambda;
     int32_t sentinel;       // index of the opposite side's all-zero sentinel row (= n_opp_rows)
+    int32_t flags;          // SOLVE_FLAG_* (diagnostics only; 0 in production)
 };
+// Diagnostic: skip the k x k solve after the Gram (stores the Gram diagonal instead) -- used by
+// tools/kbench.py to split a launch's time into Gram and solve. Never set on the product path.
+constexpr int32_t SOLVE_FLAG_SKIP_SOLVE = 1;
+constexpr int32_t SOLVE_FLAG_SKIP_REFINE = 2;   // diagnostic: no refinement step (accuracy experiments)
 
 struct SqErrArgs {
     const Task* tasks;      // FULL + PARTIAL tasks (they cover every entry exactly once)

@@ -533,6 +533,16 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
     };
     float x[C];
     solve_vec(b0, x);
+    if (a.flags & SOLVE_FLAG_SKIP_REFINE) {   // diagnostics only
+        if (g == 0) {
+            using VT = typename VecC<C>::type;
+            VT o;
+#pragma unroll
+            for (int b = 0; b < C; ++b) o[b] = (C * j + b < a.k) ? x[b] * scol[b] : 0.f;
+            *(VT*)(out + C * j) = o;
+        }
+        return;
+    }
 
     // ---- one refinement step: r = b - A x over the kept upper tiles (A_IJ and A_IJ^T), x += A^{-1} r ----
     wave_sync();
@@ -675,7 +685,25 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             // and the accumulators come out in exactly the layout of the f32 path (tile (b1, b2) holds
             // G[C*i + b1][C*j' + b2]), so the solve, the partial slots and the REDUCE pass are shared.
             // Padding entries gather the sentinel zero row with rating 0, so the last block needs no mask.
-            auto split_step = [&](const VT (&y)[B], const Idx& x) {
+            typedef int i32x4 __attribute__((ext_vector_type(4)));
+            struct Cols { i32x4 i[2]; };
+            struct Rats { f32x4 r[2]; };
+            auto load_cols = [&](int blk, Cols& x) {
+                const int32_t* c = cb + (int64_t)blk * BLOCK_ENTRIES;
+                x.i[0] = *(const i32x4*)c;
+                x.i[1] = *(const i32x4*)(c + 4);
+            };
+            auto load_rats = [&](int blk, Rats& x) {
+                const float* r = rb + (int64_t)blk * BLOCK_ENTRIES;
+                x.r[0] = *(const f32x4*)r;
+                x.r[1] = *(const f32x4*)(r + 4);
+            };
+            auto gather_blk = [&](const Cols& x, VT (&y)[B]) {
+#pragma unroll
+                for (int t = 0; t < B; ++t)
+                    y[t] = *(const VT*)(obase + (uint32_t)x.i[t >> 2][t & 3] * (uint32_t)(KP * sizeof(float)));
+            };
+            auto split_step = [&](const VT (&y)[B], const Rats& x) {
                 u32x4 H[C], M[C], L[C];
 #pragma unroll
                 for (int b = 0; b < C; ++b)
@@ -705,25 +733,80 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
 #pragma unroll
                     for (int c = 0; c < C; ++c) acc.rhs[c] += x.r[t >> 2][t & 3] * y[t][c];
             };
-            if (nblk > 0) {
-                Idx x_c, x_n;
-                VT y_c[B], y_n[B];
-                load_idx(0, x_c);
-                load_idx(nblk > 1 ? 1 : 0, x_n);
-                gather(x_c, y_c);
-                for (int b = 0; b + 1 < nblk; ++b) {
-                    Idx x_nn;
-                    load_idx(b + 2 < nblk ? b + 2 : nblk - 1, x_nn);   // clamped: always a valid address
-                    gather(x_n, y_n);
+            // Two blocks per trip with ping-pong buffers (no register rotation): column indices are loaded two
+            // blocks ahead of their gathers' use, gathers and ratings one block ahead of their MFMAs.
+            // Invariant at the loop top: Y0/R0 in flight for block b, I1 = columns of b+1, I0 = columns of b+2.
+            if (C > 4 && nblk > 0) {
+                // KP = 128 (1 wave per SIMD, 144 accumulator registers): one staging set, rotated
+                Cols Ic, In;
+                Rats Rc, Rn;
+                VT Yc[B], Yn[B];
+                const int lastb = nblk - 1;
+                load_cols(0, Ic);
+                load_cols(min(1, lastb), In);
+                gather_blk(Ic, Yc);
+                load_rats(0, Rc);
+                for (int b = 0; b < lastb; ++b) {
+                    gather_blk(In, Yn);
+                    load_rats(b + 1, Rn);
+                    load_cols(min(b + 2, lastb), In);
                     __builtin_amdgcn_sched_barrier(0);
-                    split_step(y_c, x_c);
+                    split_step(Yc, Rc);
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int t = 0; t < B; ++t) y_c[t] = y_n[t];
-                    x_c = x_n;
-                    x_n = x_nn;
+                    for (int t = 0; t < B; ++t) Yc[t] = Yn[t];
+                    Rc = Rn;
                 }
-                split_step(y_c, x_c);
+                split_step(Yc, Rc);
+            } else if (MINW >= 3 && nblk > 0) {
+                // 3 waves per SIMD (short rows from an L2-resident table, e.g. the user side): one staging
+                // set and no gather prefetch -- the third wave hides the latency instead (<= 168 VGPRs).
+                Cols Ic, In;
+                Rats Rc;
+                VT Y[B];
+                const int lastb = nblk - 1;
+                load_cols(0, Ic);
+                for (int b = 0; b < nblk; ++b) {
+                    load_cols(min(b + 1, lastb), In);
+                    gather_blk(Ic, Y);
+                    load_rats(b, Rc);
+                    split_step(Y, Rc);
+                    Ic = In;
+                }
+            } else if (nblk > 0) {
+                Cols I0, I1;
+                Rats R0, R1;
+                VT Y0[B], Y1[B];
+                const int lastb = nblk - 1;
+                load_cols(0, I0);
+                load_cols(min(1, lastb), I1);
+                gather_blk(I0, Y0);
+                load_rats(0, R0);
+                load_cols(min(2, lastb), I0);
+                int b = 0;
+                for (; b + 2 < nblk; b += 2) {
+                    gather_blk(I1, Y1);
+                    load_rats(b + 1, R1);
+                    load_cols(min(b + 3, lastb), I1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    split_step(Y0, R0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    gather_blk(I0, Y0);
+                    load_rats(b + 2, R0);
+                    load_cols(min(b + 4, lastb), I0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    split_step(Y1, R1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (nblk - b == 2) {
+                    gather_blk(I1, Y1);
+                    load_rats(b + 1, R1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    split_step(Y0, R0);
+                    split_step(Y1, R1);
+                } else {
+                    split_step(Y0, R0);
+                }
             }
         } else if constexpr (C > 4) {
             // KP = 128: 288 MFMAs per block, so half a block of prefetch (4 gathered rows per lane in
@@ -812,6 +895,14 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
         return;
     }
 
+    if (a.flags & SOLVE_FLAG_SKIP_SOLVE) {   // diagnostics (kbench): Gram only
+        float* out = (float*)a.out + (a.row_offset + tk.row) * (int64_t)KP;
+        if (lane < 16) {
+#pragma unroll
+            for (int b = 0; b < C; ++b) out[C * lane + b] = acc.g[tile_index<C>(b, b)][0] + acc.rhs[b];
+        }
+        return;
+    }
     if constexpr (tiles_in_lds<C>()) {
         LdsTiles T{tiles_lds[wave] + lane};
         RegStore<C> A0;
@@ -1017,6 +1108,7 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA, 1>(a, s);
         } else if (path == Path::MFMA_SPLIT) {
             if (kp == 32) return launch_solve_t<float, 32, Path::MFMA_SPLIT, 2>(a, s);
+            if (kp == 64 && min_waves >= 3) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 3>(a, s);
             if (kp == 64) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2>(a, s);
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1>(a, s);
         } else {
