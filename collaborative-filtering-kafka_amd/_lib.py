@@ -64,6 +64,8 @@ SIGNATURES = [
     ("als_write_factors", _i, [_vp, _i, _i64, _i64, _vp, _i64]),
     ("als_read_factors", _i, [_vp, _i, _i64, _i64, _vp, _i64]),
     ("als_solve_half", _i, [_vp, _i, _f]),
+    ("als_set_chunks", _i, [_vp, _i, _i, _pi64]),
+    ("als_solve_half_chunk", _i, [_vp, _i, _f, _i]),
     ("als_sq_error", _i, [_vp, _i, _pd, _pi64]),
     ("als_synchronize", _i, [_vp]),
     ("als_set_timing", _i, [_vp, _i]),

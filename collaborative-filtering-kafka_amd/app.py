@@ -27,7 +27,8 @@ from .engine import ALSEngine, Dataset, SIDE_MOVIE, SIDE_USER
 class ALSApp:
     def __init__(self, num_partitions: int, num_features: int, als_lambda: float, num_als_iterations: int,
                  num_movies: int | None = None, num_users: int | None = None, *, precision: str = "f32",
-                 seed: int = 42, device: int = 0, rank: int = 0, world_size: int = 1, group=None):
+                 seed: int = 42, device: int = 0, rank: int = 0, world_size: int = 1, group=None,
+                 overlap_chunks: int = 4):
         self.NUM_PARTITIONS = num_partitions
         self.NUM_FEATURES = num_features
         self.ALS_LAMBDA = float(np.float32(als_lambda))     # Float.parseFloat (ALSAppRunner.java:19)
@@ -43,6 +44,10 @@ class ALSApp:
         self.engine = None
         self.ds = None
         self.info = [None, None]
+        # user half on > 1 GPU: solve in `overlap_chunks` row ranges and all-gather each range while the
+        # next one is solved (1 = one launch, then one all-gather)
+        self.overlap_chunks = max(1, int(overlap_chunks))
+        self.chunk_slots = None
 
     # -------------------------------------------------------------------------------------------------
     def setup(self, ds: Dataset, check_duplicates: bool = True, engine_factory=None) -> "ALSApp":
@@ -72,6 +77,16 @@ class ALSApp:
             eng.alloc_factors(side, blk["n_slots"])
             eng.set_block(side, blk["row_ptr"], blk["col"], blk["ratings"], blk["row_offset"], opp["n_slots"])
             self.info[side] = {k: blk[k] for k in ("n_rows", "row_offset", "nnz", "slots_per_shard", "n_slots")}
+        if self.world > 1 and self.overlap_chunks > 1:
+            S = self.info[SIDE_USER]["slots_per_shard"]
+            n = self.info[SIDE_USER]["n_rows"]
+            Sc = -(-S // self.overlap_chunks)
+            starts = [min(c * Sc, S) for c in range(self.overlap_chunks + 1)]
+            # chunk c = slots [starts[c], starts[c+1]) of every shard; this rank solves its rows there
+            self.chunk_slots = [(starts[c], starts[c + 1]) for c in range(self.overlap_chunks)
+                                if starts[c + 1] > starts[c]]
+            bounds = [0] + [min(hi, n) for _, hi in self.chunk_slots]
+            eng.set_chunks(SIDE_USER, bounds)
         u0 = ds.init_user_factors(self.NUM_FEATURES, self.seed, self.world)
         eng.write_factors(SIDE_USER, u0)
         self.engine = eng
@@ -79,10 +94,20 @@ class ALSApp:
         return self
 
     # -------------------------------------------------------------------------------------------------
+    def _stream_ordered(self) -> bool:
+        """RCCL ("nccl") orders its kernels after the work already queued on the current stream. gloo on CUDA
+        tensors reads them with host-side copies, so the engine's stream is drained before each collective."""
+        import torch.distributed as dist
+        if not hasattr(self, "_ordered"):
+            self._ordered = dist.get_backend(self.group) == "nccl"
+        return self._ordered
+
     def _allgather(self, side: int):
         if self.world == 1:
             return
         import torch.distributed as dist
+        if not self._stream_ordered():
+            self.engine.synchronize()
         S = self.info[side]["slots_per_shard"]
         full = self.engine.factors[side]            # [G*S + 1, kp]: last row = sentinel, not exchanged
         dist.all_gather_into_tensor(full[:self.world * S], full[self.rank * S:(self.rank + 1) * S], group=self.group)
@@ -94,8 +119,23 @@ class ALSApp:
 
     def user_half(self):
         """UFeatureCalculator-i over this rank's users + all-gather (user-features-(i+1) topic)."""
-        self.engine.solve_half(SIDE_USER, self.ALS_LAMBDA)
-        self._allgather(SIDE_USER)
+        if self.chunk_slots is None:
+            self.engine.solve_half(SIDE_USER, self.ALS_LAMBDA)
+            self._allgather(SIDE_USER)
+            return
+        # chunk c's all-gather (RCCL stream, ordered after chunk c's solve) overlaps chunk c+1's solve
+        import torch.distributed as dist
+        S = self.info[SIDE_USER]["slots_per_shard"]
+        U = self.engine.factors[SIDE_USER]
+        works = []
+        for c, (lo, hi) in enumerate(self.chunk_slots):
+            self.engine.solve_half_chunk(SIDE_USER, self.ALS_LAMBDA, c)
+            if not self._stream_ordered():
+                self.engine.synchronize()
+            outs = [U[g * S + lo:g * S + hi] for g in range(self.world)]
+            works.append(dist.all_gather(outs, outs[self.rank], group=self.group, async_op=True))
+        for w in works:
+            w.wait()
 
     def iteration(self):
         self.movie_half()

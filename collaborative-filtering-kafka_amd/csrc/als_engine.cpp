@@ -49,6 +49,10 @@ struct Block {
     int32_t n_tasks = 0, n_reduce = 0, n_slots = 0;
     int min_waves = 2;              // MFMA variant occupancy target chosen from the work plan
     double* d_task_se = nullptr;    // per-task squared-error partials
+    std::vector<Task> h_tasks, h_reduce;   // host copies of the work plan (chunking re-sorts them)
+    Task* d_ctasks = nullptr;       // chunk-major FULL + PARTIAL tasks (LPT inside each chunk)
+    Task* d_creduce = nullptr;      // chunk-major REDUCE tasks
+    std::vector<int32_t> coff, croff;   // chunk c = d_ctasks[coff[c], coff[c+1]), d_creduce[croff[c], ...)
 };
 
 struct TimingRec {
@@ -105,6 +109,8 @@ void free_block(Block& b) {
     (void)hipFree(b.d_tasks);
     (void)hipFree(b.d_reduce);
     (void)hipFree(b.d_task_se);
+    (void)hipFree(b.d_ctasks);
+    (void)hipFree(b.d_creduce);
     b = Block();
 }
 
@@ -313,9 +319,8 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
     // Many short tasks (user side: ~200 ratings, one 64x64 solve each) are bound by the solve's VALU work
     // and gain from a third wave per SIMD; long chunks (movie side) are MFMA-bound and prefer 2 waves
     // without register spills (measured on the Netflix-shape workload, tools/kbench.py).
-    // split-bf16 Gram: 3 waves/SIMD (no gather prefetch) measured 2-3% faster than 2 waves with ping-pong
-    // prefetch on both sides of the Netflix-shape workload (tools/kbench.py); the f32 MFMA path prefers 2.
-    blk.min_waves = e->min_waves > 0 ? e->min_waves : (e->path == Path::MFMA_SPLIT ? 3 : 2);
+    // (the split-bf16 path has one variant: 2 waves/SIMD with the ping-pong gather prefetch)
+    blk.min_waves = e->min_waves > 0 ? e->min_waves : 2;
     auto up = [&](void** dst, const void* src, size_t bytes) -> int {
         if (bytes == 0) return ALS_OK;
         hipError_t st = hipMalloc(dst, bytes);
@@ -330,6 +335,8 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
     if ((r = up((void**)&blk.d_tasks, tasks.data(), tasks.size() * sizeof(Task)))) return r;
     if ((r = up((void**)&blk.d_reduce, reduce.data(), reduce.size() * sizeof(Task)))) return r;
     if (!tasks.empty()) HIP_TRY(hipMalloc((void**)&blk.d_task_se, tasks.size() * sizeof(double)));
+    blk.h_tasks = std::move(tasks);
+    blk.h_reduce = std::move(reduce);
     // Partial workspace sized for the larger side.
     const size_t need = (size_t)slots * cfk::partial_words_per_lane(e->precision, e->kp, e->path) * 64 * e->elem();
     if (need > e->partial_bytes) {
@@ -423,11 +430,12 @@ int als_read_factors(als_engine* e, int side, int64_t row0, int64_t n_rows, void
     return ALS_OK;
 }
 
-int als_solve_half(als_engine* e, int side, float lambda) {
-    if (int r = check_engine(e)) return r;
-    if (int r = check_side(side)) return r;
+namespace {
+
+// One half (or one chunk of it): the FULL + PARTIAL launch, then the REDUCE launch.
+int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_t n_tasks, const Task* reduce,
+                int32_t n_reduce) {
     Block& b = e->blk[side];
-    if (!b.set) return fail(ALS_ERR_STATE, "als_solve_half: no block set for side %d", side);
     const Factors& self = e->fac[side];
     const Factors& opp = e->fac[1 - side];
     if (!self.ptr || !opp.ptr) return fail(ALS_ERR_STATE, "als_solve_half: factor matrices not allocated/bound");
@@ -440,8 +448,8 @@ int als_solve_half(als_engine* e, int side, float lambda) {
     if (!(lambda >= 0.f)) return fail(ALS_ERR_INVALID_ARGUMENT, "lambda must be >= 0");
     HIP_TRY(hipSetDevice(e->device));
     cfk::SolveArgs a{};
-    a.tasks = b.d_tasks;
-    a.n_tasks = b.n_tasks;
+    a.tasks = tasks;
+    a.n_tasks = n_tasks;
     a.k = e->k;
     a.col = b.d_col;
     a.rat = b.d_rat;
@@ -466,9 +474,9 @@ int als_solve_half(als_engine* e, int side, float lambda) {
     }
     HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves));
     if (e->timing) HIP_TRY(hipEventRecord(rec.ev[1], e->stream));
-    if (b.n_reduce > 0) {
-        a.tasks = b.d_reduce;
-        a.n_tasks = b.n_reduce;
+    if (n_reduce > 0) {
+        a.tasks = reduce;
+        a.n_tasks = n_reduce;
         HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves));
     }
     if (e->timing) {
@@ -476,6 +484,70 @@ int als_solve_half(als_engine* e, int side, float lambda) {
         e->pending.push_back(rec);
     }
     return ALS_OK;
+}
+
+}  // namespace
+
+int als_solve_half(als_engine* e, int side, float lambda) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    Block& b = e->blk[side];
+    if (!b.set) return fail(ALS_ERR_STATE, "als_solve_half: no block set for side %d", side);
+    return launch_half(e, side, lambda, b.d_tasks, b.n_tasks, b.d_reduce, b.n_reduce);
+}
+
+int als_set_chunks(als_engine* e, int side, int n_chunks, const int64_t* row_bounds) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    Block& b = e->blk[side];
+    if (!b.set) return fail(ALS_ERR_STATE, "als_set_chunks: no block set for side %d", side);
+    if (n_chunks < 1 || !row_bounds) return fail(ALS_ERR_INVALID_ARGUMENT, "n_chunks must be >= 1 with row_bounds");
+    if (row_bounds[0] != 0 || row_bounds[n_chunks] != b.n_rows)
+        return fail(ALS_ERR_INVALID_ARGUMENT, "row_bounds must run from 0 to n_rows (%lld)", (long long)b.n_rows);
+    for (int c = 0; c < n_chunks; ++c)
+        if (row_bounds[c + 1] < row_bounds[c]) return fail(ALS_ERR_INVALID_ARGUMENT, "row_bounds not monotone");
+    auto chunk_of = [&](int32_t row) {
+        return (int)(std::upper_bound(row_bounds, row_bounds + n_chunks + 1, (int64_t)row) - row_bounds) - 1;
+    };
+    // stable partition by chunk keeps the longest-first order inside every chunk
+    auto split = [&](const std::vector<Task>& in, std::vector<Task>& out, std::vector<int32_t>& off) {
+        std::vector<std::vector<Task>> per(n_chunks);
+        for (const Task& t : in) per[chunk_of(t.row)].push_back(t);
+        off.assign(n_chunks + 1, 0);
+        out.clear();
+        for (int c = 0; c < n_chunks; ++c) {
+            out.insert(out.end(), per[c].begin(), per[c].end());
+            off[c + 1] = (int32_t)out.size();
+        }
+    };
+    std::vector<Task> ct, cr;
+    split(b.h_tasks, ct, b.coff);
+    split(b.h_reduce, cr, b.croff);
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    (void)hipFree(b.d_ctasks);
+    (void)hipFree(b.d_creduce);
+    b.d_ctasks = b.d_creduce = nullptr;
+    if (!ct.empty()) {
+        HIP_TRY(hipMalloc((void**)&b.d_ctasks, ct.size() * sizeof(Task)));
+        HIP_TRY(hipMemcpy(b.d_ctasks, ct.data(), ct.size() * sizeof(Task), hipMemcpyHostToDevice));
+    }
+    if (!cr.empty()) {
+        HIP_TRY(hipMalloc((void**)&b.d_creduce, cr.size() * sizeof(Task)));
+        HIP_TRY(hipMemcpy(b.d_creduce, cr.data(), cr.size() * sizeof(Task), hipMemcpyHostToDevice));
+    }
+    return ALS_OK;
+}
+
+int als_solve_half_chunk(als_engine* e, int side, float lambda, int chunk) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    Block& b = e->blk[side];
+    if (!b.set || b.coff.empty()) return fail(ALS_ERR_STATE, "als_solve_half_chunk: no chunks set for side %d", side);
+    if (chunk < 0 || chunk + 1 >= (int)b.coff.size())
+        return fail(ALS_ERR_INVALID_ARGUMENT, "chunk %d out of range (%d chunks)", chunk, (int)b.coff.size() - 1);
+    return launch_half(e, side, lambda, b.d_ctasks + b.coff[chunk], b.coff[chunk + 1] - b.coff[chunk],
+                       b.d_creduce + b.croff[chunk], b.croff[chunk + 1] - b.croff[chunk]);
 }
 
 int als_sq_error(als_engine* e, int side, double* sum_sq_error, int64_t* count) {

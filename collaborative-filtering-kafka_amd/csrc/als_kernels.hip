@@ -758,21 +758,6 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                     Rc = Rn;
                 }
                 split_step(Yc, Rc);
-            } else if (MINW >= 3 && nblk > 0) {
-                // 3 waves per SIMD (short rows from an L2-resident table, e.g. the user side): one staging
-                // set and no gather prefetch -- the third wave hides the latency instead (<= 168 VGPRs).
-                Cols Ic, In;
-                Rats Rc;
-                VT Y[B];
-                const int lastb = nblk - 1;
-                load_cols(0, Ic);
-                for (int b = 0; b < nblk; ++b) {
-                    load_cols(min(b + 1, lastb), In);
-                    gather_blk(Ic, Y);
-                    load_rats(b, Rc);
-                    split_step(Y, Rc);
-                    Ic = In;
-                }
             } else if (nblk > 0) {
                 Cols I0, I1;
                 Rats R0, R1;
@@ -1108,7 +1093,6 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA, 1>(a, s);
         } else if (path == Path::MFMA_SPLIT) {
             if (kp == 32) return launch_solve_t<float, 32, Path::MFMA_SPLIT, 2>(a, s);
-            if (kp == 64 && min_waves >= 3) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 3>(a, s);
             if (kp == 64) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2>(a, s);
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1>(a, s);
         } else {

@@ -227,6 +227,14 @@ class ALSEngine:
         """MFeatureCalculator (side='movie') / UFeatureCalculator (side='user') for every row of the block."""
         call("als_solve_half", self._h, _side(side), float(np.float32(lam)))
 
+    def set_chunks(self, side, row_bounds):
+        """Split the side's block into row-range chunks (local rows; row_bounds[0] = 0, [-1] = n_rows)."""
+        b = np.ascontiguousarray(row_bounds, np.int64)
+        call("als_set_chunks", self._h, _side(side), len(b) - 1, ptr(b, ctypes.c_int64))
+
+    def solve_half_chunk(self, side, lam: float, chunk: int):
+        call("als_solve_half_chunk", self._h, _side(side), float(np.float32(lam)), int(chunk))
+
     def sq_error(self, side="movie"):
         se = ctypes.c_double()
         cnt = ctypes.c_int64()

@@ -94,6 +94,14 @@ int als_read_factors(als_engine* e, int side, int64_t row0, int64_t n_rows, void
  * for the whole partition. Asynchronous on the engine's stream. */
 int als_solve_half(als_engine* e, int side, float lambda);
 
+/* Row-range chunks of a half (multi-GPU overlap). als_set_chunks splits `side`'s block into n_chunks
+ * ranges of its local rows, row_bounds[0] = 0 <= ... <= row_bounds[n_chunks] = n_rows; the union of the
+ * chunk launches is exactly als_solve_half. Lets the caller all-gather chunk c of the updated shard over
+ * RCCL while chunk c+1 is solved -- the per-partition fan-out of the reference's feature topics
+ * (ALSApp.java:105-148) overlapped with compute. Replaces any previous chunking of that side. */
+int als_set_chunks(als_engine* e, int side, int n_chunks, const int64_t* row_bounds);
+int als_solve_half_chunk(als_engine* e, int side, float lambda, int chunk);
+
 /* Sum of (r - x_row . y_col)^2 over the block's observed ratings and their count (the RMSE/MSE
  * reduction of scripts/calculate_mse.py:78-90 computed on the device from the factors). Synchronous. */
 int als_sq_error(als_engine* e, int side, double* sum_sq_error, int64_t* count);

@@ -1,4 +1,4 @@
-"""CPU rehearsal of the multi-GPU path with torch.distributed + gloo, world_size 2 and 3.
+"""CPU rehearsal of the multi-GPU path with torch.distributed + gloo, world_size 2, 3 and 4.
 
 The per-shard solve is injected (an oracle-backed stand-in with the ALSEngine interface): what is under
 test here is the product's distributed driver -- id % G sharding into slot order, the per-half
@@ -56,13 +56,25 @@ class OracleShardEngine:
         out = self.oracle.update_side(s, opp, lam, "f64", 1)
         self.factors[side][off:off + len(out)] = torch.from_numpy(out)
 
+    def set_chunks(self, side, bounds):
+        self.chunks = [(int(bounds[c]), int(bounds[c + 1])) for c in range(len(bounds) - 1)]
+
+    def solve_half_chunk(self, side, lam, c):
+        rp, col, rat, off, n_opp = self.blocks[side]
+        lo, hi = self.chunks[c]
+        opp = self.factors[1 - side][:n_opp].numpy()
+        sub = rp[lo:hi + 1] - rp[lo]
+        s = self.oracle.Side(ids=np.arange(hi - lo), row_ptr=sub, col=col[rp[lo]:rp[hi]], ratings=rat[rp[lo]:rp[hi]])
+        out = self.oracle.update_side(s, opp, lam, "f64", 1)
+        self.factors[side][off + lo:off + hi] = torch.from_numpy(out)
+
     def sq_error(self, side):
         rp, col, rat, off, n_opp = self.blocks[0]
         s = self.oracle.Side(ids=np.arange(len(rp) - 1), row_ptr=rp, col=col, ratings=rat)
         return self.oracle.sq_error(s, self.factors[0][off:off + len(rp) - 1].numpy(), self.factors[1][:n_opp].numpy())
 
 
-def _worker(rank, world, port, path, out_dir):
+def _worker(rank, world, port, path, out_dir, chunks=4):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -72,7 +84,7 @@ def _worker(rank, world, port, path, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ds = cfk.Dataset.load_netflix(path)
-    app = cfk.ALSApp(4, 10, 0.05, 3, precision="f64", seed=42, rank=rank, world_size=world)
+    app = cfk.ALSApp(4, 10, 0.05, 3, precision="f64", seed=42, rank=rank, world_size=world, overlap_chunks=chunks)
     app.setup(ds, engine_factory=OracleShardEngine)
     app.run()
     U, M = app.factors()
@@ -89,10 +101,12 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_driver_matches_single_process(cfk, oracle_mod, tiny_path, tmp_path, world):
+@pytest.mark.parametrize("world,chunks", [(2, 1), (2, 4), (3, 3), (4, 7)])
+def test_sharded_driver_matches_single_process(cfk, oracle_mod, tiny_path, tmp_path, world, chunks):
+    """chunks > 1: the user half is solved in row-range chunks whose all-gathers (async, list form) overlap
+    the next chunk's solve."""
     import torch.multiprocessing as mp
-    mp.spawn(_worker, args=(world, _free_port(), tiny_path, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), tiny_path, str(tmp_path), chunks), nprocs=world, join=True)
     m, u, r = oracle_mod.parse_netflix(tiny_path)
     b = oracle_mod.build_blocks(m, u, r)
     Uo, Mo = oracle_mod.run_als(b, 10, 0.05, 3, seed=42, precision="f64")

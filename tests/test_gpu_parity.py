@@ -213,3 +213,61 @@ def test_cli_app_end_to_end(tmp_path, oracle_mod, tiny_path):
     assert oracle_mod.mse_from_csv(tiny_path, str(csvs[0])) == pytest.approx(float(g["mse"]), rel=1e-6)
     res = subprocess.run([app, "4", "10", "0.05", "10", tiny_path, "1000", "302"], capture_output=True, text=True)
     assert res.returncode != 0 and "would wait forever" in res.stderr
+
+
+def test_chunked_user_half_bitwise_equal(cfk, oracle_mod):
+    """als_set_chunks / als_solve_half_chunk (the multi-GPU overlap path) reproduce als_solve_half exactly."""
+    ds, b = _synthetic(cfk, oracle_mod)
+    blk = ds.shard_block(1)
+    F = np.random.default_rng(5).random((len(b.movie.ids), 64)).astype(np.float32)
+    whole = _one_half(cfk, 1, blk, F, 64, "f32", len(b.movie.ids))
+    eng = cfk.ALSEngine(64, "f32")
+    eng.use_torch_stream()
+    eng.alloc_factors(0, len(b.movie.ids))
+    eng.alloc_factors(1, blk["n_rows"])
+    eng.set_block(1, blk["row_ptr"], blk["col"], blk["ratings"], 0, len(b.movie.ids))
+    eng.write_factors(0, F)
+    n = blk["n_rows"]
+    bounds = [0, n // 5, n // 5, n // 2, n]          # includes an empty chunk
+    eng.set_chunks(1, bounds)
+    for c in range(len(bounds) - 1):
+        eng.solve_half_chunk(1, LAM, c)
+    got = eng.read_factors(1, 0, n)
+    eng.close()
+    assert np.array_equal(got, whole)
+
+
+def _gloo_gpu_worker(rank, world, port, path, out_dir):
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    import __graft_entry__
+    cfk = __graft_entry__.load_package()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ds = cfk.Dataset.load_netflix(path)
+    app = cfk.ALSApp(4, 10, LAM, 10, 426, 302, precision="f64", seed=42, device=0, rank=rank, world_size=world,
+                     overlap_chunks=3)
+    app.setup(ds)
+    app.run()
+    U, M = app.factors()
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), U=U, M=M, mse=app.mse())
+    dist.destroy_process_group()
+
+
+def test_sharded_two_ranks_on_one_gpu(tmp_path, tiny_path):
+    """The real HIP engine under the sharded driver: 2 ranks (both on cuda:0; gloo carries the all-gathers of
+    CUDA tensors, RCCL needs one GPU per rank) with the chunked user half -> the golden fp64 result."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_gloo_gpu_worker, args=(2, port, tiny_path, str(tmp_path)), nprocs=2, join=True)
+    g = _golden("tiny")
+    for rank in range(2):
+        res = np.load(os.path.join(tmp_path, f"rank{rank}.npz"))
+        assert max_rel(res["U"], g["U"]) <= 1e-6 and max_rel(res["M"], g["M"]) <= 1e-6
+        assert abs(float(res["mse"]) - float(g["mse"])) / float(g["mse"]) <= 1e-6
