@@ -257,8 +257,21 @@ int als_dataset_from_ratings(int64_t n, const int32_t* movie_ids, const int32_t*
     return ALS_OK;
 }
 
-int als_dataset_synthetic_netflix(int64_t n_users, int64_t n_movies, int64_t nnz, uint64_t seed, int nthreads,
-                                  als_dataset** out) {
+}  // extern "C"
+
+namespace {
+
+// Shape of a synthetic rating matrix: log-normal user activity (mu, sigma of the log, per-user cap; scaled to
+// exactly nnz) and item popularity w(rank) over a seeded random rank order.
+struct SynthSpec {
+    double mu, sigma;
+    int64_t cap;
+    double rank_offset, exponent;     // w(rank) = (rank + 1 + rank_offset)^-exponent
+    uint64_t perm_salt;
+};
+
+int synthesize(const SynthSpec& sp, int64_t n_users, int64_t n_movies, int64_t nnz, uint64_t seed, int nthreads,
+               als_dataset** out) {
     if (!out) return report(fail(ALS_ERR_INVALID_ARGUMENT, "out is NULL"));
     *out = nullptr;
     if (n_users < 1 || n_movies < 1 || n_users > INT32_MAX - 1 || n_movies > INT32_MAX - 1)
@@ -267,9 +280,9 @@ int als_dataset_synthetic_netflix(int64_t n_users, int64_t n_movies, int64_t nnz
         return report(fail(ALS_ERR_INVALID_ARGUMENT, "nnz must be in [max(n_users, n_movies), n_users*n_movies/2]"));
     if (nthreads <= 0) nthreads = (int)std::max(1u, std::thread::hardware_concurrency());
     nthreads = std::min(nthreads, 64);
-    // --- user degrees: log-normal (median 96, mean 208.2 at Netflix scale), scaled to sum to nnz ---
-    const double mu = std::log(96.0), sigma = std::sqrt(2.0 * std::log(208.2 / 96.0));
-    const int64_t cap = std::min<int64_t>(17653, n_movies);
+    const double mu = sp.mu, sigma = sp.sigma;
+    const int64_t cap = std::min<int64_t>(sp.cap, n_movies);
+    if (cap * n_users < nnz) return report(fail(ALS_ERR_INVALID_ARGUMENT, "nnz exceeds n_users * per-user cap"));
     std::vector<int64_t> deg(n_users);
     {
         Rng rng(mix64(seed ^ 0xDE6DE6ULL));
@@ -296,14 +309,14 @@ int als_dataset_synthetic_netflix(int64_t n_users, int64_t n_movies, int64_t nnz
             else if (tot > nnz && deg[u] > 1) { --deg[u]; --tot; }
         }
     }
-    // --- movie popularity: w(rank) ~ (rank + 320)^-1.85 over a seeded random rank order ---
+    // --- item popularity: w(rank) = (rank + 1 + offset)^-exponent over a seeded random rank order ---
     std::vector<double> w(n_movies);
     std::vector<int32_t> perm(n_movies);
     std::iota(perm.begin(), perm.end(), 0);
     {
-        Rng rng(mix64(seed ^ 0x30F1EULL));
+        Rng rng(mix64(seed ^ sp.perm_salt));
         for (int64_t i = n_movies - 1; i > 0; --i) std::swap(perm[i], perm[rng.below(i + 1)]);
-        for (int64_t r = 0; r < n_movies; ++r) w[perm[r]] = std::pow((double)(r + 1) + 320.0, -1.85);
+        for (int64_t r = 0; r < n_movies; ++r) w[perm[r]] = std::pow((double)(r + 1) + sp.rank_offset, -sp.exponent);
     }
     // alias table (Vose)
     std::vector<double> prob(n_movies);
@@ -432,6 +445,27 @@ int als_dataset_synthetic_netflix(int64_t n_users, int64_t n_movies, int64_t nnz
     }
     *out = ds.release();
     return ALS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int als_dataset_synthetic_netflix(int64_t n_users, int64_t n_movies, int64_t nnz, uint64_t seed, int nthreads,
+                                  als_dataset** out) {
+    // user degrees log-normal (median 96, mean 208.2 at Netflix scale, cap 17,653); movies (rank + 320)^-1.85
+    const SynthSpec sp{std::log(96.0), std::sqrt(2.0 * std::log(208.2 / 96.0)), 17653, 320.0, 1.85, 0x30F1EULL};
+    return synthesize(sp, n_users, n_movies, nnz, seed, nthreads, out);
+}
+
+int als_dataset_synthetic_powerlaw(int64_t n_users, int64_t n_items, int64_t nnz, uint64_t seed, int nthreads,
+                                   als_dataset** out) {
+    // user activity log-normal with sigma 1.5 and mean nnz / n_users; item popularity ~ rank^-1 (Zipf);
+    // per-user cap n_items / 10 (the heaviest users and items are the load-balance stress)
+    const double sigma = 1.5, mean = (double)nnz / (double)std::max<int64_t>(1, n_users);
+    const SynthSpec sp{std::log(mean) - 0.5 * sigma * sigma, sigma, std::max<int64_t>(1, n_items / 10), 0.0, 1.0,
+                       0x9A11ULL};
+    return synthesize(sp, n_users, n_items, nnz, seed, nthreads, out);
 }
 
 int als_dataset_destroy(als_dataset* ds) {

@@ -244,8 +244,9 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
 
     // Padded, block-interleaved device in-block (see cfk::block_position): every row starts on a
     // 32-entry block; padding entries point at the sentinel zero row (col = n_opp_rows) with rating 0.
-    if ((n_opp_rows + 1) * (int64_t)e->kp * (int64_t)e->elem() > INT32_MAX)
-        return fail(ALS_ERR_UNSUPPORTED, "opposite factor matrix exceeds 2 GiB (32-bit gather offsets)");
+    if (n_opp_rows >= INT32_MAX) return fail(ALS_ERR_UNSUPPORTED, "n_opp_rows must be < 2^31-1 (int32 column indices)");
+    if ((n_opp_rows + 1) * (int64_t)e->kp * (int64_t)e->elem() > (int64_t)UINT32_MAX)
+        return fail(ALS_ERR_UNSUPPORTED, "opposite factor matrix exceeds 4 GiB (32-bit gather offsets)");
     std::vector<int32_t> col(nnz_padded, (int32_t)n_opp_rows);
     std::vector<float> rat(nnz_padded, 0.f);
     std::vector<int64_t> begin(n_rows + 1);

@@ -661,7 +661,8 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             x.r[0] = *(const f32x4*)r;
             x.r[1] = *(const f32x4*)(r + 4);
         };
-        // unconditional: padding entries index the sentinel zero row; 32-bit byte offsets (host-checked)
+        // unconditional: padding entries index the sentinel zero row; 32-bit unsigned byte offsets (host-checked:
+        // opposite table <= 4 GiB, e.g. 16.7M rows at k = 64)
         const char* obase = (const char*)(opp + C * j);
         auto gather = [&](const Idx& x, VT (&y)[B]) {
 #pragma unroll

@@ -60,6 +60,14 @@ class Dataset:
         call("als_dataset_synthetic_netflix", n_users, n_movies, nnz, seed, nthreads, ctypes.byref(h))
         return cls(h.value)
 
+    @classmethod
+    def synthetic_powerlaw(cls, n_users=10_000_000, n_items=1_000_000, nnz=2_000_000_000, seed=0xA15,
+                           nthreads=0) -> "Dataset":
+        """BASELINE configs[4]: log-normal user activity (sigma 1.5), Zipf item popularity."""
+        h = ctypes.c_void_p()
+        call("als_dataset_synthetic_powerlaw", n_users, n_items, nnz, seed, nthreads, ctypes.byref(h))
+        return cls(h.value)
+
     def close(self):
         if self._h and self._h.value:
             _lib.lib().als_dataset_destroy(self._h)

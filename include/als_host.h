@@ -42,6 +42,12 @@ int als_dataset_from_ratings(int64_t n, const int32_t* movie_ids, const int32_t*
  * ratings. Ids are 1..n. Arrival order is movie-major (like the Netflix files). nthreads <= 0: all cores. */
 int als_dataset_synthetic_netflix(int64_t n_users, int64_t n_movies, int64_t nnz, uint64_t seed, int nthreads,
                                   als_dataset** out);
+/* Synthetic power-law data (BASELINE.json configs[4]: 10M users x 1M items x 2B ratings): user activity
+ * log-normal (sigma 1.5, mean nnz / n_users, cap n_items / 10), item popularity ~ rank^-1 over a seeded rank
+ * order -- a few items carry millions of ratings (the split-row load-balance stress). Same guarantees as
+ * above (exact nnz, no duplicate pairs, every entity rated, ids 1..n, movie-major arrival order). */
+int als_dataset_synthetic_powerlaw(int64_t n_users, int64_t n_items, int64_t nnz, uint64_t seed, int nthreads,
+                                   als_dataset** out);
 int als_dataset_destroy(als_dataset* ds);
 
 int als_dataset_counts(const als_dataset* ds, int64_t* n_movies, int64_t* n_users, int64_t* nnz);
