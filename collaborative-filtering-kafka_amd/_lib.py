@@ -14,7 +14,8 @@ import os
 import torch  # noqa: F401  (must precede dlopen of libcfk_als.so; see module docstring)
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "build", "libcfk_als.so")
+# CFK_ALS_LIB: another build of the same library (tools/kbench.py A/B of two builds on one box)
+LIB_PATH = os.environ.get("CFK_ALS_LIB") or os.path.join(_PKG, "build", "libcfk_als.so")
 APP_PATH = os.path.join(_PKG, "build", "als_app")
 
 ALS_OK = 0

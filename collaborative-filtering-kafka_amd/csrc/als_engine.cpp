@@ -53,6 +53,7 @@ struct Block {
     Task* d_ctasks = nullptr;       // chunk-major FULL + PARTIAL tasks (LPT inside each chunk)
     Task* d_creduce = nullptr;      // chunk-major REDUCE tasks
     std::vector<int32_t> coff, croff;   // chunk c = d_ctasks[coff[c], coff[c+1]), d_creduce[croff[c], ...)
+    bool presplit = false;          // gather a pre-split (bf16 h/m/l) copy of the opposite table
 };
 
 struct TimingRec {
@@ -83,6 +84,8 @@ struct als_engine {
     Factors fac[2];
     void* d_partials = nullptr;
     size_t partial_bytes = 0;
+    void* d_split = nullptr;        // pre-split opposite table (cfk::launch_presplit), sized for the larger need
+    size_t split_bytes = 0;
     int min_waves = 0;              // ALS_MFMA_WAVES override of the per-block occupancy choice (0 = auto)
     int32_t debug_flags = 0;        // ALS_DEBUG_SKIP_SOLVE=1 -> cfk::SOLVE_FLAG_SKIP_SOLVE (tools/kbench.py only)
     bool timing = false;
@@ -189,6 +192,7 @@ int als_engine_destroy(als_engine* e) {
     for (auto& f : e->fac)
         if (f.owned) (void)hipFree(f.ptr);
     (void)hipFree(e->d_partials);
+    (void)hipFree(e->d_split);
     for (auto& rec : e->pending)
         for (auto ev : rec.ev) (void)hipEventDestroy(ev);
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
@@ -322,6 +326,26 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
     // without register spills (measured on the Netflix-shape workload, tools/kbench.py).
     // (the split-bf16 path has one variant: 2 waves/SIMD with the ping-pong gather prefetch)
     blk.min_waves = e->min_waves > 0 ? e->min_waves : 2;
+    // Pre-split opposite table for the split-bf16 Gram when it stays L2-resident (<= 8 MB as h/m/l pieces,
+    // e.g. the 17,770-row movie table of the user half): 1.5x the gathered bytes from L2, ~3x fewer VALU
+    // instructions per block (measured on the Netflix-shape user half). ALS_PRESPLIT=0/1 forces it.
+    {
+        const int64_t sb = (n_opp_rows + 1) * (int64_t)cfk::PRESPLIT_ROW_BYTES;
+        bool ps = e->path == Path::MFMA_SPLIT && e->kp == 64 && sb <= (8ll << 20);
+        if (const char* env = getenv("ALS_PRESPLIT")) ps = e->path == Path::MFMA_SPLIT && e->kp == 64 && env[0] == '1';
+        if (n_opp_rows + 1 >= (1 << 24)) ps = false;   // 24-bit row offsets in the pre-split gather
+        blk.presplit = ps;
+        if (ps && (size_t)sb > e->split_bytes) {
+            HIP_TRY(hipStreamSynchronize(e->stream));
+            (void)hipFree(e->d_split);
+            e->d_split = nullptr;
+            e->split_bytes = 0;
+            hipError_t st = hipMalloc(&e->d_split, (size_t)sb);
+            if (st != hipSuccess) return fail(ALS_ERR_OUT_OF_MEMORY, "pre-split hipMalloc(%lld): %s", (long long)sb,
+                                              hipGetErrorString(st));
+            e->split_bytes = (size_t)sb;
+        }
+    }
     auto up = [&](void** dst, const void* src, size_t bytes) -> int {
         if (bytes == 0) return ALS_OK;
         hipError_t st = hipMalloc(dst, bytes);
@@ -473,12 +497,16 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
         }
         HIP_TRY(hipEventRecord(rec.ev[0], e->stream));
     }
-    HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves));
+    if (b.presplit) {
+        HIP_TRY(cfk::launch_presplit((const float*)opp.ptr, e->d_split, b.n_opp_rows + 1, e->stream));
+        a.opp_split = e->d_split;
+    }
+    HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves, b.presplit));
     if (e->timing) HIP_TRY(hipEventRecord(rec.ev[1], e->stream));
     if (n_reduce > 0) {
         a.tasks = reduce;
         a.n_tasks = n_reduce;
-        HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves));
+        HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves, b.presplit));
     }
     if (e->timing) {
         HIP_TRY(hipEventRecord(rec.ev[2], e->stream));

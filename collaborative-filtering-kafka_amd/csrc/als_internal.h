@@ -53,6 +53,7 @@ struct SolveArgs {
     float lambda;
     int32_t sentinel;       // index of the opposite side's all-zero sentinel row (= n_opp_rows)
     int32_t flags;          // SOLVE_FLAG_* (diagnostics only; 0 in production)
+    const void* opp_split;  // MFMA_SPLIT + presplit: the opposite table as bf16 h/m/l pieces (als_presplit)
 };
 // Diagnostic: skip the k x k solve after the Gram (stores the Gram diagonal instead) -- used by
 // tools/kbench.py to split a launch's time into Gram and solve. Never set on the product path.
@@ -78,7 +79,13 @@ enum class Path : int { VALU = 0, MFMA = 1, MFMA_SPLIT = 2 };
 
 // Launch helpers (defined in als_kernels.hip). Return hipSuccess or the launch error.
 // min_waves: occupancy target (waves per SIMD) of the MFMA variant (__launch_bounds__ second argument).
-hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, int min_waves);
+hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, int min_waves,
+                        bool presplit = false);
+// Pre-split of an fp32 [n_rows][64] factor table (sentinel row included) into the bf16 h/m/l piece layout
+// the presplit Gram gathers: row r, lane piece j (features 4j..4j+3) = 6 dwords at byte r*384 + j*24:
+// h(f0,f1) h(f2,f3) m(f0,f1) m(f2,f3) l(f0,f1) l(f2,f3).
+constexpr int PRESPLIT_ROW_BYTES = 384;
+hipError_t launch_presplit(const float* src, void* dst, int64_t n_rows, hipStream_t s);
 hipError_t launch_sq_error(int precision, int kp, const SqErrArgs& a, hipStream_t s);
 // Per-lane accumulator words (elements of the engine precision) of one partial slot: nacc * 64.
 int partial_words_per_lane(int precision, int kp, Path path);

@@ -40,6 +40,7 @@ typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 template <class T> struct Vec16;
 template <> struct Vec16<float> { typedef f32x4 type; static constexpr int N = 4; };
@@ -302,15 +303,13 @@ template <int L>
 __device__ __forceinline__ float row_lane_bcast(float v) {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + L, 0xf, 0xf, false));
 }
-// value of lane (G, c) at every lane (g, c): v_permlane16_swap picks the even/odd row of each row pair,
-// v_permlane32_swap the low/high pair
+// value of lane (G, c) at every lane (g, c): one ds_bpermute through the LDS crossbar (no LDS storage).
+// Measured 3-5% faster on the solve-heavy user half than the v_permlane16/32_swap pair it replaced (the
+// swaps clobber both operands, which cost register copies and hazard NOPs on every sweep step).
 template <int G>
 __device__ __forceinline__ float col_bcast(float v) {
-    const int x = __float_as_int(v);
-    const auto s16 = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-    const int y = (G & 1) ? (int)s16[1] : (int)s16[0];
-    const auto s32 = __builtin_amdgcn_permlane32_swap(y, y, false, false);
-    return __int_as_float((G & 2) ? (int)s32[1] : (int)s32[0]);
+    const int addr = ((int)(__lane_id() & 15) + 16 * G) * 4;
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
 }
 // sum over the 4 rows at each column, result in every row
 __device__ __forceinline__ float col_sum(float v) {
@@ -604,7 +603,22 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 template <int KP>
 constexpr int mfma_waves() { return WAVES; }
 
-template <int KP, int MINW, bool SPLIT>
+// fp32 table -> bf16 h/m/l pieces (PRESPLIT_ROW_BYTES per row), one thread per 16-B row piece.
+__global__ __launch_bounds__(256) void als_presplit(const float* __restrict__ src, unsigned* __restrict__ dst,
+                                                   int64_t n_pieces) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= n_pieces) return;
+    const f32x4 x = *(const f32x4*)(src + t * 4);
+    unsigned h01, m01, l01, h23, m23, l23;
+    split3(x[0], x[1], h01, m01, l01);
+    split3(x[2], x[3], h23, m23, l23);
+    unsigned* o = dst + t * 6;
+    *(u32x2*)o = u32x2{h01, h23};
+    *(u32x2*)(o + 2) = u32x2{m01, m23};
+    *(u32x2*)(o + 4) = u32x2{l01, l23};
+}
+
+template <int KP, int MINW, bool SPLIT, bool PRESPLIT = false>
 __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(SolveArgs a) {
     constexpr int C = KP / 16;
     constexpr int NW = mfma_waves<KP>();
@@ -679,7 +693,126 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
 #pragma unroll
             for (int c = 0; c < C; ++c) acc.rhs[c] += r * y[c];
         };
-        if constexpr (SPLIT) {
+        if constexpr (PRESPLIT) {
+            // Split-bf16 Gram over a PRE-SPLIT opposite table (als_presplit, once per half): lane (g, j) loads
+            // the 24-B h/m/l piece of features 4j..4j+3 of its group's 8 entries and only transposes bf16
+            // halves into the MFMA operands (v_perm_b32: 48 per block instead of ~150 split instructions).
+            // The RHS Y^T r becomes 12 more MFMAs (ratings 1..5 are exact in bf16; B[k][*] = r_k, so every
+            // column of the result holds Y_b^T r). Chosen for tables that stay L2-resident (the 17,770-row
+            // movie table the user half reads): 1.5x the gathered bytes, far fewer VALU instructions.
+            static_assert(C == 4, "pre-split Gram: KP = 64");
+            typedef int i32x4 __attribute__((ext_vector_type(4)));
+            struct Cols { i32x4 i[2]; };
+            struct Rats { f32x4 r[2]; };
+            struct Piece { unsigned w[6]; };
+            auto load_cols = [&](int blk, Cols& x) {
+                const int32_t* c = cb + (int64_t)blk * BLOCK_ENTRIES;
+                x.i[0] = *(const i32x4*)c;
+                x.i[1] = *(const i32x4*)(c + 4);
+            };
+            auto load_rats = [&](int blk, Rats& x) {
+                const float* r = rb + (int64_t)blk * BLOCK_ENTRIES;
+                x.r[0] = *(const f32x4*)r;
+                x.r[1] = *(const f32x4*)(r + 4);
+            };
+            const char* sbase = (const char*)a.opp_split + j * 24;
+            auto gather_blk = [&](const Cols& x, Piece (&y)[B]) {
+#pragma unroll
+                for (int t = 0; t < B; ++t) {
+                    // 24-bit multiply (full rate; pre-split tables are small: host-checked < 2^24 rows)
+                    const char* p = sbase + __umul24((uint32_t)x.i[t >> 2][t & 3], (uint32_t)PRESPLIT_ROW_BYTES);
+                    const u32x2 a0 = *(const u32x2*)p, a1 = *(const u32x2*)(p + 8), a2 = *(const u32x2*)(p + 16);
+                    y[t].w[0] = a0[0]; y[t].w[1] = a0[1];
+                    y[t].w[2] = a1[0]; y[t].w[3] = a1[1];
+                    y[t].w[4] = a2[0]; y[t].w[5] = a2[1];
+                }
+            };
+            f32x4 racc[C];
+#pragma unroll
+            for (int b = 0; b < C; ++b) racc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+            auto step = [&](const Piece (&y)[B], const Rats& x) {
+                u32x4 P[3][C];   // plane (h, m, l) x feature block b: entries 0..7 as bf16 pairs
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                    for (int b = 0; b < C; ++b)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            P[pl][b][q] = __builtin_amdgcn_perm(y[2 * q + 1].w[2 * pl + (b >> 1)],
+                                                                y[2 * q].w[2 * pl + (b >> 1)],
+                                                                (b & 1) ? 0x07060302u : 0x05040100u);
+                u32x4 R;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) R[q] = pk_bf16(x.r[q >> 1][2 * (q & 1)], x.r[q >> 1][2 * (q & 1) + 1]);
+#pragma unroll
+                for (int b1 = 0; b1 < C; ++b1)
+#pragma unroll
+                    for (int b2 = b1; b2 < C; ++b2) {
+                        f32x4 t = acc.g[tile_index<C>(b1, b2)];
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[1][b1]), as_bf16x8(P[1][b2]), t, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[0][b1]), as_bf16x8(P[2][b2]), t, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[2][b1]), as_bf16x8(P[0][b2]), t, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[0][b1]), as_bf16x8(P[1][b2]), t, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[1][b1]), as_bf16x8(P[0][b2]), t, 0, 0, 0);
+                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[0][b1]), as_bf16x8(P[0][b2]), t, 0, 0, 0);
+                        acc.g[tile_index<C>(b1, b2)] = t;
+                    }
+#pragma unroll
+                for (int b = 0; b < C; ++b) {
+                    f32x4 t = racc[b];
+                    t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[2][b]), as_bf16x8(R), t, 0, 0, 0);
+                    t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[1][b]), as_bf16x8(R), t, 0, 0, 0);
+                    t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[0][b]), as_bf16x8(R), t, 0, 0, 0);
+                    racc[b] = t;
+                }
+            };
+            if (nblk > 0) {
+                Cols I0, I1;
+                Rats R0, R1;
+                Piece Y0[B], Y1[B];
+                const int lastb = nblk - 1;
+                load_cols(0, I0);
+                load_cols(min(1, lastb), I1);
+                gather_blk(I0, Y0);
+                load_rats(0, R0);
+                load_cols(min(2, lastb), I0);
+                int b = 0;
+                for (; b + 2 < nblk; b += 2) {
+                    gather_blk(I1, Y1);
+                    load_rats(b + 1, R1);
+                    load_cols(min(b + 3, lastb), I1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    step(Y0, R0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    gather_blk(I0, Y0);
+                    load_rats(b + 2, R0);
+                    load_cols(min(b + 4, lastb), I0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    step(Y1, R1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (nblk - b == 2) {
+                    gather_blk(I1, Y1);
+                    load_rats(b + 1, R1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    step(Y0, R0);
+                    step(Y1, R1);
+                } else {
+                    step(Y0, R0);
+                }
+            }
+            // RHS tiles (row i of block b = feature 4i + b, every column equal) -> the per-lane partial layout
+            // of the other paths: lane (0, j) holds feature 4j + b, the other rows zero (col_sum restores it)
+            wave_sync();
+            if (j == 0) {
+#pragma unroll
+                for (int b = 0; b < C; ++b) *(f32x4*)(buf + 16 * b + 4 * g) = racc[b];
+            }
+            wave_sync();
+#pragma unroll
+            for (int b = 0; b < C; ++b) acc.rhs[b] = (g == 0) ? buf[16 * b + j] : 0.f;
+            wave_sync();
+        } else if constexpr (SPLIT) {
             // Split-bf16 Gram: one v_mfma_f32_16x16x32_bf16 consumes a whole 32-entry block. Lane (g, j)
             // holds A[i = j][k = 8g + t] = y_t[C*j + b] (its own gathered piece, component b, entry t of its
             // group): with the interleaved feature order (f = C*i + b) the operands need no lane movement,
@@ -1039,14 +1172,14 @@ __global__ __launch_bounds__(256) void als_sq_error_kernel(SqErrArgs a) {
 
 int blocks_for(int n_tasks) { return (n_tasks + WAVES - 1) / WAVES; }
 
-template <class T, int KP, Path P, int MINW = 1>
+template <class T, int KP, Path P, int MINW = 1, bool PRESPLIT = false>
 hipError_t launch_solve_t(const SolveArgs& a, hipStream_t s) {
     if (a.n_tasks <= 0) return hipSuccess;
     constexpr int bytes = WAVES * WaveLds<T, KP, P>::BYTES;
     if constexpr (P == Path::MFMA || P == Path::MFMA_SPLIT) {
         static_assert(std::is_same<T, float>::value, "MFMA paths are fp32");
         constexpr int nw = mfma_waves<KP>();
-        als_solve_mfma<KP, MINW, P == Path::MFMA_SPLIT><<<(a.n_tasks + nw - 1) / nw, 64 * nw, 0, s>>>(a);
+        als_solve_mfma<KP, MINW, P == Path::MFMA_SPLIT, PRESPLIT><<<(a.n_tasks + nw - 1) / nw, 64 * nw, 0, s>>>(a);
     } else {
         static bool attr = false;
         if (!attr) {
@@ -1085,7 +1218,15 @@ int partial_words_per_lane(int precision, int kp, Path path) {
     return kp * kp / 64 + 1;
 }
 
-hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, int min_waves) {
+hipError_t launch_presplit(const float* src, void* dst, int64_t n_rows, hipStream_t s) {
+    const int64_t pieces = n_rows * 16;
+    if (pieces <= 0) return hipSuccess;
+    als_presplit<<<(unsigned)((pieces + 255) / 256), 256, 0, s>>>(src, (unsigned*)dst, pieces);
+    return hipGetLastError();
+}
+
+hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, int min_waves,
+                        bool presplit) {
     if (precision == 0) {
         if (path == Path::MFMA) {
             if (kp == 32) return launch_solve_t<float, 32, Path::MFMA, 2>(a, s);
@@ -1094,6 +1235,7 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA, 1>(a, s);
         } else if (path == Path::MFMA_SPLIT) {
             if (kp == 32) return launch_solve_t<float, 32, Path::MFMA_SPLIT, 2>(a, s);
+            if (kp == 64 && presplit) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2, true>(a, s);
             if (kp == 64) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2>(a, s);
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1>(a, s);
         } else {
