@@ -3,5 +3,5 @@
 The directory name contains dashes, so it is loaded under the module name ``cfk_amd`` (see
 ``load_package`` in ``__graft_entry__.py``). The native library is ``build/libcfk_als.so``.
 """
-from .engine import ALSEngine, Dataset, factor_stride, u01, write_prediction_csv  # noqa: F401
+from .engine import ALSEngine, Dataset, factor_stride, u01, write_prediction_csv, write_prediction_matrix_csv  # noqa: F401
 from .app import ALSApp  # noqa: F401

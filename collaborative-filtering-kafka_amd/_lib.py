@@ -67,6 +67,7 @@ SIGNATURES = [
     ("als_solve_half", _i, [_vp, _i, _f]),
     ("als_set_chunks", _i, [_vp, _i, _i, _pi64]),
     ("als_solve_half_chunk", _i, [_vp, _i, _f, _i]),
+    ("als_predict", _i, [_vp, _pi64, _i64, _pi64, _i64, _pf]),
     ("als_sq_error", _i, [_vp, _i, _pd, _pi64]),
     ("als_synchronize", _i, [_vp]),
     ("als_set_timing", _i, [_vp, _i]),
@@ -88,6 +89,7 @@ SIGNATURES = [
     ("als_dataset_init_user_factors", _i, [_vp, _i, _u64, _i, _pf, _i64, _i64]),
     ("als_u01", _f, [_u64, _i64, ctypes.c_int32]),
     ("als_write_prediction_csv", _i, [ctypes.c_char_p, _pf, _i64, _i64, _pf, _i64, _i64, _i]),
+    ("als_write_prediction_matrix_csv", _i, [ctypes.c_char_p, _pf, _i64, _i64]),
 ]
 
 

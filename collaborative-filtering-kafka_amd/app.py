@@ -157,6 +157,11 @@ class ALSApp:
         M = self.engine.read_factors(SIDE_MOVIE)
         return U[self.ds.slots(SIDE_USER, self.world)], M[self.ds.slots(SIDE_MOVIE, self.world)]
 
+    def prediction_matrix(self) -> np.ndarray:
+        """FeatureCollector.calculatePredictionMatrix (FeatureCollector.java:90-101): users x movies, both in
+        ascending id order, computed on the GPU from the (gathered) factor replicas."""
+        return self.engine.predict(self.ds.slots(SIDE_USER, self.world), self.ds.slots(SIDE_MOVIE, self.world))
+
     def sq_error(self):
         """Sum of squared errors over all observed ratings (all ranks) and the rating count."""
         se, cnt = self.engine.sq_error(SIDE_MOVIE)

@@ -67,9 +67,9 @@ int main(int argc, char** argv) {
         return 0;
     }
     long long P, K, N, NM, NU;
-    if (!parse_int(argv[1], 1, INT_MAX, P) || !parse_int(argv[2], 1, 64, K) || !parse_int(argv[4], 0, INT_MAX, N) ||
+    if (!parse_int(argv[1], 1, INT_MAX, P) || !parse_int(argv[2], 1, 128, K) || !parse_int(argv[4], 0, INT_MAX, N) ||
         !parse_int(argv[6], 0, INT_MAX, NM) || !parse_int(argv[7], 0, INT_MAX, NU)) {
-        fprintf(stderr, "als_app: bad integer argument (NUM_FEATURES must be 1..64)\n");
+        fprintf(stderr, "als_app: bad integer argument (NUM_FEATURES must be 1..128; 1..64 with --precision f64)\n");
         return 1;
     }
     char* end = nullptr;
@@ -162,23 +162,18 @@ int main(int argc, char** argv) {
     printf("ALS: %lld iterations in %.3f s (%.3e ratings/s per iteration); MSE %.6f RMSE %.6f\n", N, secs,
            N > 0 ? (double)nnz * N / secs : 0.0, cnt ? se / cnt : 0.0, cnt ? std::sqrt(se / cnt) : 0.0);
 
-    // FeatureCollector: factors in ascending id order (slot order for one shard).
+    // FeatureCollector: factors in ascending id order (slot order for one shard); U M^T on the GPU with the
+    // collector's Java-float dot, then the EJML CSV text on the host.
     printf("Start Prediction Matrix Computation at %s\n", java_timestamp().c_str());
-    std::vector<float> U((size_t)nu * k), M((size_t)nm * k);
-    if (precision == ALS_F32) {
-        if (als_read_factors(e, ALS_SIDE_USER, 0, nu, U.data(), k) != ALS_OK) return die("read");
-        if (als_read_factors(e, ALS_SIDE_MOVIE, 0, nm, M.data(), k) != ALS_OK) return die("read");
-    } else {
-        std::vector<double> u64((size_t)nu * k), m64((size_t)nm * k);
-        if (als_read_factors(e, ALS_SIDE_USER, 0, nu, u64.data(), k) != ALS_OK) return die("read");
-        if (als_read_factors(e, ALS_SIDE_MOVIE, 0, nm, m64.data(), k) != ALS_OK) return die("read");
-        for (size_t i = 0; i < U.size(); ++i) U[i] = (float)u64[i];
-        for (size_t i = 0; i < M.size(); ++i) M[i] = (float)m64[i];
-    }
+    std::vector<int64_t> urows(nu), mrows(nm);
+    for (int64_t i = 0; i < nu; ++i) urows[i] = i;
+    for (int64_t i = 0; i < nm; ++i) mrows[i] = i;
+    std::vector<float> pred((size_t)nu * (size_t)nm);
+    if (als_predict(e, urows.data(), nu, mrows.data(), nm, pred.data()) != ALS_OK) return die("predict");
     mkdir(outdir.c_str(), 0755);
     const std::string path = outdir + "/prediction_matrix_" + java_timestamp();
     printf("Done at %s\n", java_timestamp().c_str());
-    if (als_write_prediction_csv(path.c_str(), U.data(), nu, k, M.data(), nm, k, k) != ALS_OK) return die("csv");
+    if (als_write_prediction_matrix_csv(path.c_str(), pred.data(), nu, nm) != ALS_OK) return die("csv");
     printf("Prediction matrix: %s\n", path.c_str());
     als_engine_destroy(e);
     als_dataset_destroy(ds);

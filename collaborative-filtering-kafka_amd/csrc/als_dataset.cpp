@@ -593,23 +593,21 @@ int als_dataset_init_user_factors(const als_dataset* ds, int num_features, uint6
     return ALS_OK;
 }
 
-int als_write_prediction_csv(const char* path, const float* U, int64_t n_users, int64_t ldu, const float* M,
-                             int64_t n_movies, int64_t ldm, int num_features) {
-    if (!path || (n_users > 0 && !U) || (n_movies > 0 && !M) || num_features < 1 || ldu < num_features ||
-        ldm < num_features)
-        return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));
+}  // extern "C"
+
+namespace {
+
+// EJML MatrixIO.saveDenseCSV of the widened matrix; cell(i, j) yields the fp32 prediction.
+template <class Cell>
+int write_csv(const char* path, int64_t n_users, int64_t n_movies, Cell cell) {
     FILE* f = fopen(path, "wb");
     if (!f) return report(fail(ALS_ERR_IO, "cannot create %s", path));
     fprintf(f, "%lld %lld real\n", (long long)n_users, (long long)n_movies);
     std::string line;
     for (int64_t i = 0; i < n_users; ++i) {
         line.clear();
-        const float* x = U + i * ldu;
         for (int64_t j = 0; j < n_movies; ++j) {
-            const float* y = M + j * ldm;
-            float total = 0.f;   // MatrixMatrixMult_FDRM.multTransB: sequential fp32 dot
-            for (int c = 0; c < num_features; ++c) total += x[c] * y[c];
-            line += java_double((double)total);
+            line += java_double((double)cell(i, j));
             line.push_back(' ');
         }
         line.push_back('\n');
@@ -620,6 +618,30 @@ int als_write_prediction_csv(const char* path, const float* U, int64_t n_users, 
     }
     if (fclose(f) != 0) return report(fail(ALS_ERR_IO, "close failed: %s", path));
     return ALS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int als_write_prediction_csv(const char* path, const float* U, int64_t n_users, int64_t ldu, const float* M,
+                             int64_t n_movies, int64_t ldm, int num_features) {
+    if (!path || (n_users > 0 && !U) || (n_movies > 0 && !M) || num_features < 1 || ldu < num_features ||
+        ldm < num_features)
+        return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));
+    return write_csv(path, n_users, n_movies, [&](int64_t i, int64_t j) {
+        const float* x = U + i * ldu;
+        const float* y = M + j * ldm;
+        float total = 0.f;   // MatrixMatrixMult_FDRM.multTransB: sequential fp32 dot
+        for (int c = 0; c < num_features; ++c) total += x[c] * y[c];
+        return total;
+    });
+}
+
+int als_write_prediction_matrix_csv(const char* path, const float* P, int64_t n_users, int64_t n_movies) {
+    if (!path || n_users < 0 || n_movies < 0 || (n_users > 0 && n_movies > 0 && !P))
+        return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));
+    return write_csv(path, n_users, n_movies, [&](int64_t i, int64_t j) { return P[i * n_movies + j]; });
 }
 
 }  // extern "C"

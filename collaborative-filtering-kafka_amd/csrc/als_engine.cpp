@@ -579,6 +579,47 @@ int als_solve_half_chunk(als_engine* e, int side, float lambda, int chunk) {
                        b.d_creduce + b.croff[chunk], b.croff[chunk + 1] - b.croff[chunk]);
 }
 
+int als_predict(als_engine* e, const int64_t* user_rows, int64_t n_users, const int64_t* movie_rows,
+                int64_t n_movies, float* host_out) {
+    if (int r = check_engine(e)) return r;
+    if (n_users < 0 || n_movies < 0) return fail(ALS_ERR_INVALID_ARGUMENT, "negative counts");
+    if (n_users == 0 || n_movies == 0) return ALS_OK;
+    if (!user_rows || !movie_rows || !host_out) return fail(ALS_ERR_INVALID_ARGUMENT, "NULL pointer");
+    const Factors& U = e->fac[ALS_SIDE_USER];
+    const Factors& M = e->fac[ALS_SIDE_MOVIE];
+    if (!U.ptr || !M.ptr) return fail(ALS_ERR_STATE, "als_predict: factor matrices not allocated/bound");
+    for (int64_t i = 0; i < n_users; ++i)
+        if (user_rows[i] < 0 || user_rows[i] >= U.n_rows) return fail(ALS_ERR_INVALID_ARGUMENT, "user row out of range");
+    for (int64_t i = 0; i < n_movies; ++i)
+        if (movie_rows[i] < 0 || movie_rows[i] >= M.n_rows) return fail(ALS_ERR_INVALID_ARGUMENT, "movie row out of range");
+    if ((n_users + 15) / 16 > 65535) return fail(ALS_ERR_UNSUPPORTED, "at most 1,048,560 users per call (call per user range)");
+    HIP_TRY(hipSetDevice(e->device));
+    int64_t *d_u = nullptr, *d_m = nullptr;
+    float* d_out = nullptr;
+    const size_t ob = (size_t)n_users * (size_t)n_movies * sizeof(float);
+    auto cleanup = [&]() {
+        (void)hipFree(d_u);
+        (void)hipFree(d_m);
+        (void)hipFree(d_out);
+    };
+    hipError_t st = hipMalloc((void**)&d_u, n_users * sizeof(int64_t));
+    if (st == hipSuccess) st = hipMalloc((void**)&d_m, n_movies * sizeof(int64_t));
+    if (st == hipSuccess) st = hipMalloc((void**)&d_out, ob);
+    if (st != hipSuccess) {
+        cleanup();
+        return fail(ALS_ERR_OUT_OF_MEMORY, "als_predict: hipMalloc: %s", hipGetErrorString(st));
+    }
+    st = hipMemcpyAsync(d_u, user_rows, n_users * sizeof(int64_t), hipMemcpyHostToDevice, e->stream);
+    if (st == hipSuccess) st = hipMemcpyAsync(d_m, movie_rows, n_movies * sizeof(int64_t), hipMemcpyHostToDevice, e->stream);
+    if (st == hipSuccess)
+        st = cfk::launch_predict(e->precision, U.ptr, M.ptr, e->kp, e->k, d_u, n_users, d_m, n_movies, d_out, e->stream);
+    if (st == hipSuccess) st = hipMemcpyAsync(host_out, d_out, ob, hipMemcpyDeviceToHost, e->stream);
+    if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
+    cleanup();
+    if (st != hipSuccess) return fail(ALS_ERR_DEVICE, "als_predict: %s", hipGetErrorString(st));
+    return ALS_OK;
+}
+
 int als_sq_error(als_engine* e, int side, double* sum_sq_error, int64_t* count) {
     if (int r = check_engine(e)) return r;
     if (int r = check_side(side)) return r;

@@ -1170,6 +1170,36 @@ __global__ __launch_bounds__(256) void als_sq_error_kernel(SqErrArgs a) {
     if (lane == 0) a.task_se[tid] = se;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Collector prediction matrix (FeatureCollector.java:90-101): P[u][m] = sum_f U[u][f] * M[m][f] in fp32 with
+// Java float semantics -- each product and each partial sum rounded separately, features in order (EJML
+// MatrixMatrixMult_FDRM.multTransB's sequential dot; no FMA contraction) -- so that the CSV digits are the
+// reference's. 16 x 16 cells per workgroup, the 16 + 16 factor rows staged in LDS.
+// ---------------------------------------------------------------------------------------------------
+template <class T>
+__global__ __launch_bounds__(256) void als_predict_kernel(const T* __restrict__ U, const T* __restrict__ M, int kp,
+                                                          int k, const int64_t* __restrict__ urows, int64_t n_u,
+                                                          const int64_t* __restrict__ mrows, int64_t n_m,
+                                                          float* __restrict__ out) {
+    __shared__ float su[16][129], sm[16][129];
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int64_t u0 = (int64_t)blockIdx.y * 16, m0 = (int64_t)blockIdx.x * 16;
+    for (int i = threadIdx.x; i < 16 * k; i += 256) {
+        const int r = i / k, f = i % k;
+        su[r][f] = (u0 + r < n_u) ? (float)U[urows[u0 + r] * kp + f] : 0.f;   // f64 factors reach the
+        sm[r][f] = (m0 + r < n_m) ? (float)M[mrows[m0 + r] * kp + f] : 0.f;   // collector as floats
+    }
+    __syncthreads();
+    const int64_t u = u0 + ty, m = m0 + tx;
+    if (u >= n_u || m >= n_m) return;
+    float total = 0.f;
+    {
+#pragma clang fp contract(off)
+        for (int f = 0; f < k; ++f) total = total + su[ty][f] * sm[tx][f];   // rounded product, rounded sum
+    }
+    out[u * n_m + m] = total;
+}
+
 int blocks_for(int n_tasks) { return (n_tasks + WAVES - 1) / WAVES; }
 
 template <class T, int KP, Path P, int MINW = 1, bool PRESPLIT = false>
@@ -1216,6 +1246,19 @@ int partial_words_per_lane(int precision, int kp, Path path) {
         return (c * (c + 1) / 2) * 4 + c;
     }
     return kp * kp / 64 + 1;
+}
+
+hipError_t launch_predict(int precision, const void* U, const void* M, int kp, int k, const int64_t* urows,
+                          int64_t n_u, const int64_t* mrows, int64_t n_m, float* out, hipStream_t s) {
+    if (n_u <= 0 || n_m <= 0) return hipSuccess;
+    if (k > 128 || (n_m + 15) / 16 > INT32_MAX || (n_u + 15) / 16 > 65535) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((n_m + 15) / 16), (unsigned)((n_u + 15) / 16));
+    if (precision == 0)
+        als_predict_kernel<float><<<grid, 256, 0, s>>>((const float*)U, (const float*)M, kp, k, urows, n_u, mrows, n_m, out);
+    else
+        als_predict_kernel<double><<<grid, 256, 0, s>>>((const double*)U, (const double*)M, kp, k, urows, n_u, mrows, n_m,
+                                                        out);
+    return hipGetLastError();
 }
 
 hipError_t launch_presplit(const float* src, void* dst, int64_t n_rows, hipStream_t s) {

@@ -164,6 +164,12 @@ def write_prediction_csv(path: str, U: np.ndarray, M: np.ndarray) -> None:
          M.shape[0], k, k)
 
 
+def write_prediction_matrix_csv(path: str, P: np.ndarray) -> None:
+    """The collector's CSV from an already computed prediction matrix (e.g. ALSEngine.predict)."""
+    P = np.ascontiguousarray(P, np.float32)
+    call("als_write_prediction_matrix_csv", path.encode(), ptr(P, ctypes.c_float), P.shape[0], P.shape[1])
+
+
 class ALSEngine:
     """One device engine: the in-blocks of this rank's shard of both sides + bound factor matrices."""
 
@@ -242,6 +248,15 @@ class ALSEngine:
 
     def solve_half_chunk(self, side, lam: float, chunk: int):
         call("als_solve_half_chunk", self._h, _side(side), float(np.float32(lam)), int(chunk))
+
+    def predict(self, user_rows, movie_rows) -> np.ndarray:
+        """FeatureCollector's U M^T (Java-float dots) for the given factor rows, on the GPU."""
+        ur = np.ascontiguousarray(user_rows, np.int64)
+        mr = np.ascontiguousarray(movie_rows, np.int64)
+        out = np.zeros((len(ur), len(mr)), np.float32)
+        call("als_predict", self._h, ptr(ur, ctypes.c_int64), len(ur), ptr(mr, ctypes.c_int64), len(mr),
+             ptr(out, ctypes.c_float))
+        return out
 
     def sq_error(self, side="movie"):
         se = ctypes.c_double()

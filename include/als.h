@@ -102,6 +102,14 @@ int als_solve_half(als_engine* e, int side, float lambda);
 int als_set_chunks(als_engine* e, int side, int n_chunks, const int64_t* row_bounds);
 int als_solve_half_chunk(als_engine* e, int side, float lambda, int chunk);
 
+/* FeatureCollector's prediction matrix (FeatureCollector.java:90-101) from the resident factors:
+ * host_out[u * n_movies + m] = U[user_rows[u]] . M[movie_rows[m]] as a Java float dot (fp32 products and
+ * sums rounded separately, features in order -- EJML multTransB), so the CSV written from it carries the
+ * reference's digits. Rows are factor-matrix rows (slots); pass them in ascending-id order for the
+ * collector's layout (FeatureCollector.java:72-88). Synchronous. */
+int als_predict(als_engine* e, const int64_t* user_rows, int64_t n_users, const int64_t* movie_rows,
+                int64_t n_movies, float* host_out);
+
 /* Sum of (r - x_row . y_col)^2 over the block's observed ratings and their count (the RMSE/MSE
  * reduction of scripts/calculate_mse.py:78-90 computed on the device from the factors). Synchronous. */
 int als_sq_error(als_engine* e, int side, double* sum_sq_error, int64_t* count);

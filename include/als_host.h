@@ -82,6 +82,9 @@ float als_u01(uint64_t seed, int64_t raw_id, int32_t feature);
  * followed by one space, one row per line) with Java Double.toString-style shortest round-trip values. */
 int als_write_prediction_csv(const char* path, const float* U, int64_t n_users, int64_t ldu, const float* M,
                              int64_t n_movies, int64_t ldm, int num_features);
+/* The same file from a prediction matrix already computed (e.g. on the GPU by als_predict): P row-major
+ * n_users x n_movies. */
+int als_write_prediction_matrix_csv(const char* path, const float* P, int64_t n_users, int64_t n_movies);
 
 #ifdef __cplusplus
 }

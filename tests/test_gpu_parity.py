@@ -271,3 +271,21 @@ def test_sharded_two_ranks_on_one_gpu(tmp_path, tiny_path):
         res = np.load(os.path.join(tmp_path, f"rank{rank}.npz"))
         assert max_rel(res["U"], g["U"]) <= 1e-6 and max_rel(res["M"], g["M"]) <= 1e-6
         assert abs(float(res["mse"]) - float(g["mse"])) / float(g["mse"]) <= 1e-6
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_gpu_collector_prediction_matrix(cfk, tiny_path, tmp_path, precision):
+    """FeatureCollector's U M^T on the GPU (als_predict) is bitwise the Java-float dot of the factors, and the
+    CSV written from it is byte-identical to the host writer's (FeatureCollector.java:90-110)."""
+    from test_host import java_float_dots
+    ds = cfk.Dataset.load_netflix(tiny_path)
+    app = cfk.ALSApp(4, 10, LAM, 2, 426, 302, precision=precision, seed=42).setup(ds)
+    app.run()
+    U, M = app.factors()
+    P = app.prediction_matrix()
+    assert P.shape == (302, 426)
+    assert np.array_equal(P, java_float_dots(U.astype(np.float32), M.astype(np.float32)))
+    a, c = tmp_path / "a.csv", tmp_path / "c.csv"
+    cfk.write_prediction_csv(str(a), U.astype(np.float32), M.astype(np.float32))
+    cfk.write_prediction_matrix_csv(str(c), P)
+    assert a.read_bytes() == c.read_bytes()

@@ -112,6 +112,36 @@ def test_prediction_csv_matches_oracle_bytes(cfk, oracle_mod, tiny_path, tmp_pat
     assert oracle_mod.mse_from_csv(tiny_path, str(out)) == pytest.approx(ref["mse"], rel=1e-14)
 
 
+def java_float_dots(U, M):
+    """FeatureCollector's fp32 U M^T with Java float semantics: every product and partial sum rounded."""
+    U = np.asarray(U, np.float32)
+    M = np.asarray(M, np.float32)
+    total = np.zeros((U.shape[0], M.shape[0]), np.float32)
+    for f in range(U.shape[1]):
+        total = (total + np.outer(U[:, f], M[:, f]).astype(np.float32)).astype(np.float32)
+    return total
+
+
+def test_prediction_matrix_csv_writer(cfk, oracle_mod, tiny_path, tmp_path):
+    """als_write_prediction_matrix_csv(P) == als_write_prediction_csv(U, M) byte for byte when P holds the
+    Java-float dots (the GPU collector's output contract, checked bitwise in tests/test_gpu_parity.py)."""
+    m, u, r = oracle_mod.parse_netflix(tiny_path)
+    b = oracle_mod.build_blocks(m, u, r, 4)
+    U, M = oracle_mod.run_als(b, 5, 0.05, 7, seed=42)
+    a, c = tmp_path / "a.csv", tmp_path / "c.csv"
+    cfk.write_prediction_csv(str(a), U.astype(np.float32), M.astype(np.float32))
+    cfk.write_prediction_matrix_csv(str(c), java_float_dots(U, M))
+    assert a.read_bytes() == c.read_bytes()
+
+
+def test_synthetic_powerlaw_generator(cfk):
+    """configs[4] shape at small scale: exact nnz, no duplicates, every entity rated, heavy-tailed items."""
+    ds = cfk.Dataset.synthetic_powerlaw(20_000, 2_000, 2_000_000, 5, 4)
+    assert ds.counts() == (2_000, 20_000, 2_000_000) and ds.count_duplicates() == 0
+    deg = np.diff(ds.shard_block(0)["row_ptr"])
+    assert deg.min() >= 1 and deg.max() > 20 * np.median(deg)
+
+
 def test_synthetic_generator_shape(cfk):
     ds = cfk.Dataset.synthetic_netflix(n_users=20_000, n_movies=2_000, nnz=400_000, seed=5, nthreads=4)
     nm, nu, nnz = ds.counts()
