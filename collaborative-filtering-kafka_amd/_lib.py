@@ -59,6 +59,7 @@ SIGNATURES = [
     ("als_engine_set_stream", _i, [_vp, _vp]),
     ("als_factor_stride", _i, [_vp]),
     ("als_set_block", _i, [_vp, _i, _i64, _i64, _i64, _pi64, _pi32, _pi16]),
+    ("als_set_block_coo", _i, [_vp, _i, _i64, _i64, _i64, _i64, _pi32, _pi32, _pi16]),
     ("als_alloc_factors", _i, [_vp, _i, _i64]),
     ("als_bind_factors", _i, [_vp, _i, _vp, _i64]),
     ("als_factors_device_ptr", _i, [_vp, _i, _ppv, _pi64]),
@@ -85,6 +86,7 @@ SIGNATURES = [
     ("als_dataset_count_duplicates", _i, [_vp, _pi64]),
     ("als_dataset_shard_info", _i, [_vp, _i, _i, _i, _pi64, _pi64, _pi64, _pi64, _pi64]),
     ("als_dataset_shard_block", _i, [_vp, _i, _i, _i64, _pi64, _pi32, _pi16, _pi64]),
+    ("als_dataset_shard_coo", _i, [_vp, _i, _i, _i64, _pi32, _pi32, _pi16]),
     ("als_dataset_slots", _i, [_vp, _i, _i, _pi64]),
     ("als_dataset_init_user_factors", _i, [_vp, _i, _u64, _i, _pf, _i64, _i64]),
     ("als_u01", _f, [_u64, _i64, ctypes.c_int32]),

@@ -50,7 +50,8 @@ class ALSApp:
         self.chunk_slots = None
 
     # -------------------------------------------------------------------------------------------------
-    def setup(self, ds: Dataset, check_duplicates: bool = True, engine_factory=None) -> "ALSApp":
+    def setup(self, ds: Dataset, check_duplicates: bool = True, engine_factory=None,
+              block_build: str = "device") -> "ALSApp":
         """Blocks of this rank's shard + factor replicas + U0 (UFeatureInitializer after the EOF barrier).
 
         ``engine_factory(k, precision, device)`` replaces the HIP engine with another object of the same
@@ -72,10 +73,17 @@ class ALSApp:
             eng = engine_factory(self.NUM_FEATURES, self.precision, self.device)
         eng.use_torch_stream()
         for side in (SIDE_MOVIE, SIDE_USER):
-            blk = ds.shard_block(side, self.world, self.rank)
             opp = ds.shard_info(1 - side, self.world, self.rank)
-            eng.alloc_factors(side, blk["n_slots"])
-            eng.set_block(side, blk["row_ptr"], blk["col"], blk["ratings"], blk["row_offset"], opp["n_slots"])
+            if block_build == "device" and hasattr(eng, "set_block_coo"):
+                # block builders on the GPU: arrival-order COO -> stable radix sort by row (als_set_block_coo)
+                blk = ds.shard_coo(side, self.world, self.rank)
+                eng.alloc_factors(side, blk["n_slots"])
+                eng.set_block_coo(side, blk["n_rows"], blk["rows"], blk["cols"], blk["ratings"], blk["row_offset"],
+                                  opp["n_slots"])
+            else:
+                blk = ds.shard_block(side, self.world, self.rank)
+                eng.alloc_factors(side, blk["n_slots"])
+                eng.set_block(side, blk["row_ptr"], blk["col"], blk["ratings"], blk["row_offset"], opp["n_slots"])
             self.info[side] = {k: blk[k] for k in ("n_rows", "row_offset", "nnz", "slots_per_shard", "n_slots")}
         if self.world > 1 and self.overlap_chunks > 1:
             S = self.info[SIDE_USER]["slots_per_shard"]

@@ -562,6 +562,30 @@ int als_dataset_shard_block(const als_dataset* ds, int side, int n_shards, int64
     return ALS_OK;
 }
 
+int als_dataset_shard_coo(const als_dataset* ds, int side, int n_shards, int64_t shard, int32_t* rows,
+                          int32_t* cols, int16_t* ratings) {
+    if (!ds || (side != 0 && side != 1) || n_shards < 1 || shard < 0 || shard >= n_shards || !rows || !cols || !ratings)
+        return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));
+    const int opp = 1 - side;
+    const ShardMap ms = shard_map(ds, side, n_shards);
+    const ShardMap mo = shard_map(ds, opp, n_shards);
+    const int64_t nr = ms.count[shard];
+    const int64_t base = shard * ms.S;
+    const auto& dn = ds->dense[side];
+    const auto& dop = ds->dense[opp];
+    const int64_t n = (int64_t)dn.size();
+    int64_t p = 0;
+    for (int64_t t = 0; t < n; ++t) {   // arrival order: the order the block builder sees the ratings
+        const int64_t s = ms.slot[dn[t]];
+        if (s < base || s >= base + nr) continue;
+        rows[p] = (int32_t)(s - base);
+        cols[p] = (int32_t)mo.slot[dop[t]];
+        ratings[p] = ds->rating[t];
+        ++p;
+    }
+    return ALS_OK;
+}
+
 int als_dataset_slots(const als_dataset* ds, int side, int n_shards, int64_t* slot_of) {
     if (!ds || (side != 0 && side != 1) || n_shards < 1 || !slot_of)
         return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));

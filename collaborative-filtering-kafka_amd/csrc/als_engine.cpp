@@ -221,59 +221,39 @@ int als_engine_set_stream(als_engine* e, void* hip_stream) {
 
 int als_factor_stride(const als_engine* e) { return e ? e->kp : 0; }
 
-int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows,
-                  const int64_t* row_ptr, const int32_t* col_idx, const int16_t* ratings) {
-    if (int r = check_engine(e)) return r;
-    if (int r = check_side(side)) return r;
+}  // extern "C"
+
+namespace {
+
+int check_block_shape(als_engine* e, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows) {
     if (n_rows < 0 || row_offset < 0 || n_opp_rows < 0)
         return fail(ALS_ERR_INVALID_ARGUMENT, "negative size (n_rows=%lld row_offset=%lld n_opp_rows=%lld)",
                     (long long)n_rows, (long long)row_offset, (long long)n_opp_rows);
     if (n_rows > INT32_MAX) return fail(ALS_ERR_UNSUPPORTED, "n_rows exceeds 2^31-1");
-    if (n_rows > 0 && !row_ptr) return fail(ALS_ERR_INVALID_ARGUMENT, "row_ptr is NULL");
-    const int64_t nnz = n_rows > 0 ? row_ptr[n_rows] : 0;
-    if (n_rows > 0 && row_ptr[0] != 0) return fail(ALS_ERR_INVALID_ARGUMENT, "row_ptr[0] must be 0");
-    if (nnz > 0 && (!col_idx || !ratings)) return fail(ALS_ERR_INVALID_ARGUMENT, "col_idx/ratings NULL");
-    // Validate the block on the host: a bad index would fault the GPU.
-    int64_t nnz_padded = 0;
-    for (int64_t i = 0; i < n_rows; ++i) {
-        const int64_t d = row_ptr[i + 1] - row_ptr[i];
-        if (d < 0) return fail(ALS_ERR_INVALID_ARGUMENT, "row_ptr not monotone at row %lld", (long long)i);
-        if (d > INT32_MAX / 2) return fail(ALS_ERR_UNSUPPORTED, "row %lld has %lld entries", (long long)i, (long long)d);
-        nnz_padded += (d + cfk::BLOCK_ENTRIES - 1) / cfk::BLOCK_ENTRIES * cfk::BLOCK_ENTRIES;
-    }
-    for (int64_t t = 0; t < nnz; ++t)
-        if (col_idx[t] < 0 || col_idx[t] >= n_opp_rows)
-            return fail(ALS_ERR_INVALID_ARGUMENT, "col_idx[%lld]=%d outside [0, %lld)", (long long)t, col_idx[t],
-                        (long long)n_opp_rows);
-
-    // Padded, block-interleaved device in-block (see cfk::block_position): every row starts on a
-    // 32-entry block; padding entries point at the sentinel zero row (col = n_opp_rows) with rating 0.
     if (n_opp_rows >= INT32_MAX) return fail(ALS_ERR_UNSUPPORTED, "n_opp_rows must be < 2^31-1 (int32 column indices)");
     if ((n_opp_rows + 1) * (int64_t)e->kp * (int64_t)e->elem() > (int64_t)UINT32_MAX)
         return fail(ALS_ERR_UNSUPPORTED, "opposite factor matrix exceeds 4 GiB (32-bit gather offsets)");
-    std::vector<int32_t> col(nnz_padded, (int32_t)n_opp_rows);
-    std::vector<float> rat(nnz_padded, 0.f);
-    std::vector<int64_t> begin(n_rows + 1);
-    {
-        int64_t o = 0;
-        for (int64_t i = 0; i < n_rows; ++i) {
-            begin[i] = o;
-            const int64_t b = row_ptr[i], d = row_ptr[i + 1] - b;
-            for (int64_t t = 0; t < d; ++t) {
-                const int64_t pos = o + cfk::block_position(t);
-                col[pos] = col_idx[b + t];
-                rat[pos] = (float)ratings[b + t];
-            }
-            o += (d + cfk::BLOCK_ENTRIES - 1) / cfk::BLOCK_ENTRIES * cfk::BLOCK_ENTRIES;
-        }
-        begin[n_rows] = o;
-    }
-    // Work plan.
+    return ALS_OK;
+}
+
+// Padded entries of a row of degree d (every row starts on a 32-entry block).
+inline int64_t padded(int64_t d) { return (d + cfk::BLOCK_ENTRIES - 1) / cfk::BLOCK_ENTRIES * cfk::BLOCK_ENTRIES; }
+
+// Work plan of a block whose padded in-block (d_col / d_rat, device, already laid out) has row degrees deg[]
+// and row starts begin[]: FULL / PARTIAL / REDUCE tasks, longest first; uploads the plan, takes ownership of
+// d_col / d_rat and sizes the partial and pre-split workspaces.
+int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows, int64_t nnz,
+                 const std::vector<int64_t>& deg, const std::vector<int64_t>& begin, int32_t* d_col, float* d_rat) {
+    const int64_t nnz_padded = begin[n_rows];
+    auto drop = [&]() {
+        (void)hipFree(d_col);
+        (void)hipFree(d_rat);
+    };
     const int64_t chunk = chunk_entries(nnz_padded);
     std::vector<Task> tasks, reduce;
     int64_t slots = 0;
     for (int64_t i = 0; i < n_rows; ++i) {
-        const int64_t d = row_ptr[i + 1] - row_ptr[i];
+        const int64_t d = deg[i];
         Task t{};
         t.row = (int32_t)i;
         t.ndeg = (int32_t)d;
@@ -303,16 +283,24 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
             reduce.push_back(r);
         }
     }
-    if (slots > INT32_MAX) return fail(ALS_ERR_UNSUPPORTED, "too many partial slots");
+    if (slots > INT32_MAX || tasks.size() > (size_t)INT32_MAX) {
+        drop();
+        return fail(ALS_ERR_UNSUPPORTED, "too many tasks / partial slots");
+    }
     // Longest tasks first (LPT): the grid drains with a short tail.
     std::stable_sort(tasks.begin(), tasks.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
     std::stable_sort(reduce.begin(), reduce.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
-    if (tasks.size() > (size_t)INT32_MAX) return fail(ALS_ERR_UNSUPPORTED, "too many tasks");
 
-    HIP_TRY(hipSetDevice(e->device));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    hipError_t st0 = hipSetDevice(e->device);
+    if (st0 == hipSuccess) st0 = hipStreamSynchronize(e->stream);
+    if (st0 != hipSuccess) {
+        drop();
+        return fail(ALS_ERR_DEVICE, "set_block: %s", hipGetErrorString(st0));
+    }
     Block& blk = e->blk[side];
     free_block(blk);
+    blk.d_col = d_col;
+    blk.d_rat = d_rat;
     blk.n_rows = n_rows;
     blk.row_offset = row_offset;
     blk.n_opp_rows = n_opp_rows;
@@ -321,10 +309,7 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
     blk.n_tasks = (int32_t)tasks.size();
     blk.n_reduce = (int32_t)reduce.size();
     blk.n_slots = (int32_t)slots;
-    // Many short tasks (user side: ~200 ratings, one 64x64 solve each) are bound by the solve's VALU work
-    // and gain from a third wave per SIMD; long chunks (movie side) are MFMA-bound and prefer 2 waves
-    // without register spills (measured on the Netflix-shape workload, tools/kbench.py).
-    // (the split-bf16 path has one variant: 2 waves/SIMD with the ping-pong gather prefetch)
+    // 2 waves/SIMD (the split-bf16 path has one variant; the f32 path takes ALS_MFMA_WAVES=3 for experiments)
     blk.min_waves = e->min_waves > 0 ? e->min_waves : 2;
     // Pre-split opposite table for the split-bf16 Gram when it stays L2-resident (<= 8 MB as h/m/l pieces,
     // e.g. the 17,770-row movie table of the user half): 1.5x the gathered bytes from L2, ~3x fewer VALU
@@ -336,7 +321,6 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
         if (n_opp_rows + 1 >= (1 << 24)) ps = false;   // 24-bit row offsets in the pre-split gather
         blk.presplit = ps;
         if (ps && (size_t)sb > e->split_bytes) {
-            HIP_TRY(hipStreamSynchronize(e->stream));
             (void)hipFree(e->d_split);
             e->d_split = nullptr;
             e->split_bytes = 0;
@@ -355,8 +339,6 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
         return ALS_OK;
     };
     int r;
-    if ((r = up((void**)&blk.d_col, col.data(), col.size() * 4))) return r;
-    if ((r = up((void**)&blk.d_rat, rat.data(), rat.size() * 4))) return r;
     if ((r = up((void**)&blk.d_tasks, tasks.data(), tasks.size() * sizeof(Task)))) return r;
     if ((r = up((void**)&blk.d_reduce, reduce.data(), reduce.size() * sizeof(Task)))) return r;
     if (!tasks.empty()) HIP_TRY(hipMalloc((void**)&blk.d_task_se, tasks.size() * sizeof(double)));
@@ -374,6 +356,81 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
     }
     blk.set = true;
     return ALS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows,
+                  const int64_t* row_ptr, const int32_t* col_idx, const int16_t* ratings) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    if (int r = check_block_shape(e, n_rows, row_offset, n_opp_rows)) return r;
+    if (n_rows > 0 && !row_ptr) return fail(ALS_ERR_INVALID_ARGUMENT, "row_ptr is NULL");
+    const int64_t nnz = n_rows > 0 ? row_ptr[n_rows] : 0;
+    if (n_rows > 0 && row_ptr[0] != 0) return fail(ALS_ERR_INVALID_ARGUMENT, "row_ptr[0] must be 0");
+    if (nnz > 0 && (!col_idx || !ratings)) return fail(ALS_ERR_INVALID_ARGUMENT, "col_idx/ratings NULL");
+    // Validate the block on the host: a bad index would fault the GPU.
+    std::vector<int64_t> deg(n_rows), begin(n_rows + 1);
+    int64_t o = 0;
+    for (int64_t i = 0; i < n_rows; ++i) {
+        const int64_t d = row_ptr[i + 1] - row_ptr[i];
+        if (d < 0) return fail(ALS_ERR_INVALID_ARGUMENT, "row_ptr not monotone at row %lld", (long long)i);
+        if (d > INT32_MAX / 2) return fail(ALS_ERR_UNSUPPORTED, "row %lld has %lld entries", (long long)i, (long long)d);
+        deg[i] = d;
+        begin[i] = o;
+        o += padded(d);
+    }
+    begin[n_rows] = o;
+    for (int64_t t = 0; t < nnz; ++t)
+        if (col_idx[t] < 0 || col_idx[t] >= n_opp_rows)
+            return fail(ALS_ERR_INVALID_ARGUMENT, "col_idx[%lld]=%d outside [0, %lld)", (long long)t, col_idx[t],
+                        (long long)n_opp_rows);
+    // Padded, block-interleaved device in-block (see cfk::block_position): every row starts on a
+    // 32-entry block; padding entries point at the sentinel zero row (col = n_opp_rows) with rating 0.
+    std::vector<int32_t> col(o, (int32_t)n_opp_rows);
+    std::vector<float> rat(o, 0.f);
+    for (int64_t i = 0; i < n_rows; ++i)
+        for (int64_t t = 0; t < deg[i]; ++t) {
+            const int64_t pos = begin[i] + cfk::block_position(t);
+            col[pos] = col_idx[row_ptr[i] + t];
+            rat[pos] = (float)ratings[row_ptr[i] + t];
+        }
+    HIP_TRY(hipSetDevice(e->device));
+    int32_t* d_col = nullptr;
+    float* d_rat = nullptr;
+    if (o > 0) {
+        hipError_t st = hipMalloc((void**)&d_col, o * 4);
+        if (st == hipSuccess) st = hipMalloc((void**)&d_rat, o * 4);
+        if (st == hipSuccess) st = hipMemcpy(d_col, col.data(), o * 4, hipMemcpyHostToDevice);
+        if (st == hipSuccess) st = hipMemcpy(d_rat, rat.data(), o * 4, hipMemcpyHostToDevice);
+        if (st != hipSuccess) {
+            (void)hipFree(d_col);
+            (void)hipFree(d_rat);
+            return fail(ALS_ERR_OUT_OF_MEMORY, "in-block upload: %s", hipGetErrorString(st));
+        }
+    }
+    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat);
+}
+
+int als_set_block_coo(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows, int64_t nnz,
+                      const int32_t* rows, const int32_t* cols, const int16_t* ratings) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    if (int r = check_block_shape(e, n_rows, row_offset, n_opp_rows)) return r;
+    if (nnz < 0) return fail(ALS_ERR_INVALID_ARGUMENT, "nnz < 0");
+    if (nnz > 0 && (!rows || !cols || !ratings)) return fail(ALS_ERR_INVALID_ARGUMENT, "rows/cols/ratings NULL");
+    if (nnz >= INT32_MAX) return fail(ALS_ERR_UNSUPPORTED, "nnz per block must be < 2^31-1 (shard the side)");
+    HIP_TRY(hipSetDevice(e->device));
+    std::vector<int64_t> deg, begin;
+    int32_t* d_col = nullptr;
+    float* d_rat = nullptr;
+    std::string err;
+    const int code = cfk::build_block_device(rows, cols, ratings, nnz, n_rows, n_opp_rows, e->stream, deg, begin,
+                                             &d_col, &d_rat, err);
+    if (code != ALS_OK) return fail(code, "als_set_block_coo: %s", err.c_str());
+    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat);
 }
 
 int als_alloc_factors(als_engine* e, int side, int64_t n_total_rows) {

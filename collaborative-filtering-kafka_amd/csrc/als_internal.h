@@ -1,6 +1,8 @@
 // Internal declarations shared by the engine (als_engine.cpp) and the kernels (als_kernels.hip).
 #pragma once
 #include <cstdint>
+#include <string>
+#include <vector>
 
 #include <hip/hip_runtime.h>
 
@@ -92,6 +94,13 @@ hipError_t launch_predict(int precision, const void* U, const void* M, int kp, i
 hipError_t launch_sq_error(int precision, int kp, const SqErrArgs& a, hipStream_t s);
 // Per-lane accumulator words (elements of the engine precision) of one partial slot: nacc * 64.
 int partial_words_per_lane(int precision, int kp, Path path);
+// In-block build on the device (als_build.hip): host COO (local row, opposite slot, rating) in arrival order ->
+// stable radix sort by row -> the padded block-interleaved d_col / d_rat of als_set_block, row degrees and
+// padded row starts back on the host (for the work plan). Returns an als_status; on failure `err` says why and
+// nothing is left allocated.
+int build_block_device(const int32_t* rows, const int32_t* cols, const int16_t* ratings, int64_t nnz, int64_t n_rows,
+                       int64_t n_opp_rows, hipStream_t s, std::vector<int64_t>& deg, std::vector<int64_t>& begin,
+                       int32_t** d_col, float** d_rat, std::string& err);
 // Host-side check that a (precision, kp, path) variant is compiled in.
 bool variant_available(int precision, int kp, Path path);
 

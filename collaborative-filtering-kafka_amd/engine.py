@@ -135,6 +135,17 @@ class Dataset:
         info.update(row_ptr=rp, col=col, ratings=rat, row_ids=ids)
         return info
 
+    def shard_coo(self, side, n_shards=1, shard=0) -> dict:
+        """The shard's ratings as COO (local row, opposite slot, rating) in arrival order."""
+        info = self.shard_info(side, n_shards, shard)
+        rows = np.zeros(info["nnz"], np.int32)
+        cols = np.zeros(info["nnz"], np.int32)
+        rat = np.zeros(info["nnz"], np.int16)
+        call("als_dataset_shard_coo", self._h, _side(side), n_shards, shard, ptr(rows, ctypes.c_int32),
+             ptr(cols, ctypes.c_int32), ptr(rat, ctypes.c_int16))
+        info.update(rows=rows, cols=cols, ratings=rat)
+        return info
+
     def slots(self, side, n_shards=1) -> np.ndarray:
         side = _side(side)
         n = self.counts()[0 if side == SIDE_MOVIE else 1]
@@ -208,6 +219,14 @@ class ALSEngine:
         r = np.ascontiguousarray(ratings, np.int16)
         call("als_set_block", self._h, _side(side), len(rp) - 1, row_offset, n_opp_rows, ptr(rp, ctypes.c_int64),
              ptr(c, ctypes.c_int32), ptr(r, ctypes.c_int16))
+
+    def set_block_coo(self, side, n_rows: int, rows, cols, ratings, row_offset: int, n_opp_rows: int):
+        """Same block from arrival-order COO; the in-block sort and layout run on the GPU."""
+        r = np.ascontiguousarray(rows, np.int32)
+        c = np.ascontiguousarray(cols, np.int32)
+        v = np.ascontiguousarray(ratings, np.int16)
+        call("als_set_block_coo", self._h, _side(side), n_rows, row_offset, n_opp_rows, len(r),
+             ptr(r, ctypes.c_int32), ptr(c, ctypes.c_int32), ptr(v, ctypes.c_int16))
 
     def bind_factors(self, side, tensor: torch.Tensor):
         """Bind a [n_rows + 1, kp] tensor: rows [0, n_rows) are the factors, the last row is the engine's

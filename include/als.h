@@ -72,6 +72,13 @@ int als_factor_stride(const als_engine* e);
 int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows,
                   const int64_t* row_ptr, const int32_t* col_idx, const int16_t* ratings);
 
+/* The same block from COO triples in arrival order (rows[t] = local row, cols[t] = opposite row, ratings[t]):
+ * the stable sort into in-block order (= arrival order per row, MRatings2BlocksProcessor.java:53-69) and the
+ * padded layout are done on the GPU (radix sort by row), replacing the host-side CSR build for large data.
+ * Host pointers; results identical to als_set_block on the equivalent CSR. nnz < 2^31 per call. */
+int als_set_block_coo(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows, int64_t nnz,
+                      const int32_t* rows, const int32_t* cols, const int16_t* ratings);
+
 /* ---- factor matrices (device resident) ---------------------------------------------------------- */
 /* Engine-owned buffer of n_total_rows x stride elements (zeroed), plus one hidden all-zero sentinel row
  * after the last row (in-block padding entries gather it instead of being masked). */

@@ -67,6 +67,10 @@ int als_dataset_shard_info(const als_dataset* ds, int side, int n_shards, int sh
  * ratings[nnz], row_ids[n_rows] = raw ids (any of col/ratings/row_ids may be NULL). */
 int als_dataset_shard_block(const als_dataset* ds, int side, int n_shards, int64_t shard, int64_t* row_ptr,
                             int32_t* col_idx, int16_t* ratings, int64_t* row_ids);
+/* The same shard as COO triples in arrival order (rows = local rows, cols = opposite slots): the input of
+ * als_set_block_coo, which does the sort into in-blocks on the GPU. Arrays of shard_info's nnz entries. */
+int als_dataset_shard_coo(const als_dataset* ds, int side, int n_shards, int64_t shard, int32_t* rows,
+                          int32_t* cols, int16_t* ratings);
 /* slot_of[i] = slot of the i-th entity of `side` in ascending raw-id order. */
 int als_dataset_slots(const als_dataset* ds, int side, int n_shards, int64_t* slot_of);
 /* U0 for every user, written at its slot row (out has n_out_rows >= n_slots rows of ld >= k floats;

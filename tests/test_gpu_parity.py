@@ -289,3 +289,56 @@ def test_gpu_collector_prediction_matrix(cfk, tiny_path, tmp_path, precision):
     cfk.write_prediction_csv(str(a), U.astype(np.float32), M.astype(np.float32))
     cfk.write_prediction_matrix_csv(str(c), P)
     assert a.read_bytes() == c.read_bytes()
+
+
+@pytest.mark.parametrize("precision,k", [("f32", 64), ("f64", 10), ("f32", 10)])
+def test_device_block_build_matches_host(cfk, oracle_mod, precision, k):
+    """als_set_block_coo (GPU radix-sort block build) == als_set_block (host CSR): same work plan, bitwise
+    identical half-iteration output, on a sharded synthetic block (G = 3, shard 1) and the whole block."""
+    ds, b = _synthetic(cfk, oracle_mod)
+    for G, shard in ((1, 0), (3, 1)):
+        for side in (0, 1):
+            csr = ds.shard_block(side, G, shard)
+            coo = ds.shard_coo(side, G, shard)
+            opp = ds.shard_info(1 - side, G, shard)["n_slots"]
+            F = np.random.default_rng(3).random((opp, k)).astype(np.float32 if precision == "f32" else np.float64)
+            outs, stats = [], []
+            for mode in ("host", "device"):
+                eng = cfk.ALSEngine(k, precision)
+                eng.use_torch_stream()
+                eng.alloc_factors(1 - side, opp)
+                eng.alloc_factors(side, csr["n_slots"])
+                if mode == "host":
+                    eng.set_block(side, csr["row_ptr"], csr["col"], csr["ratings"], csr["row_offset"], opp)
+                else:
+                    eng.set_block_coo(side, coo["n_rows"], coo["rows"], coo["cols"], coo["ratings"], coo["row_offset"],
+                                      opp)
+                eng.write_factors(1 - side, F)
+                eng.solve_half(side, LAM)
+                outs.append(eng.read_factors(side))
+                stats.append(eng.block_stats(side))
+                eng.close()
+            assert stats[0] == stats[1]
+            assert np.array_equal(outs[0], outs[1]), (G, shard, side)
+
+
+def test_device_block_build_edge_cases(cfk):
+    from cfk_amd._lib import ALSError
+    eng = cfk.ALSEngine(16, "f32")
+    eng.use_torch_stream()
+    eng.alloc_factors(0, 3)
+    eng.alloc_factors(1, 4)
+    eng.set_block_coo(0, 3, np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0, np.int16), 0, 4)   # empty
+    assert eng.block_stats(0)["nnz_padded"] == 0
+    # rows 0 and 2 rated, row 1 empty (zero factor), arrival order kept
+    eng.set_block_coo(0, 3, np.array([2, 0, 2], np.int32), np.array([1, 3, 0], np.int32), np.array([5, 1, 2], np.int16), 0, 4)
+    assert eng.block_stats(0)["nnz_padded"] == 64
+    eng.write_factors(1, np.ones((4, 16), np.float32))
+    eng.solve_half(0, LAM)
+    out = eng.read_factors(0)
+    assert np.all(out[1] == 0) and np.all(np.isfinite(out))
+    with pytest.raises(ALSError, match="ALS_ERR_INVALID_ARGUMENT"):
+        eng.set_block_coo(0, 3, np.array([3], np.int32), np.array([0], np.int32), np.array([1], np.int16), 0, 4)
+    with pytest.raises(ALSError, match="ALS_ERR_INVALID_ARGUMENT"):
+        eng.set_block_coo(0, 3, np.array([0], np.int32), np.array([4], np.int32), np.array([1], np.int16), 0, 4)
+    eng.close()

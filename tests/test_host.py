@@ -184,3 +184,17 @@ def test_cli_arguments_missing_message():
     app = os.path.join(ROOT, "collaborative-filtering-kafka_amd", "build", "als_app")
     res = subprocess.run([app, "4", "10"], capture_output=True, text=True)
     assert res.returncode == 0 and "ARGUMENTS MISSING" in res.stdout      # ALSAppRunner.java:11-14
+
+
+def test_shard_coo_is_arrival_order_of_the_in_blocks(cfk, tiny_path):
+    """A stable sort of the COO export by row reproduces the host CSR in-blocks exactly (the contract the GPU
+    block build of als_set_block_coo relies on)."""
+    ds = cfk.Dataset.load_netflix(tiny_path)
+    for G, shard in ((1, 0), (3, 1), (4, 3)):
+        for side in (0, 1):
+            csr = ds.shard_block(side, G, shard)
+            coo = ds.shard_coo(side, G, shard)
+            order = np.argsort(coo["rows"], kind="stable")
+            assert np.array_equal(np.bincount(coo["rows"], minlength=csr["n_rows"]), np.diff(csr["row_ptr"]))
+            assert np.array_equal(coo["cols"][order], csr["col"])
+            assert np.array_equal(coo["ratings"][order], csr["ratings"])
