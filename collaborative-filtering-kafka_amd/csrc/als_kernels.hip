@@ -341,7 +341,7 @@ __device__ __forceinline__ void sweep_tile(f32x4& a, int lane) {
         constexpr int p = decltype(P_)::value;
         constexpr int pg = p >> 2, pr = p & 3;
         const float nrd = __builtin_amdgcn_rcpf(-bcast(a[pr], 16 * pg + p));   // -1 / d
-        const bool piv = opaque(lane) == 16 * pg + p;
+        const bool piv = lane == 16 * pg + p;   // 16 lane masks, CSE-d across the 4 diagonal tiles (SGPRs)
         a[pr] = piv ? a[pr] - 1.f : a[pr];
         const float t = col_bcast<pg>(a[pr]) * nrd;                   // a[p][c] (d - 1 at c = p) * (-1/d)
         f32x4 cp;
