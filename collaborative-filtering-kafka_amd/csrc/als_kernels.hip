@@ -88,6 +88,7 @@ __device__ __forceinline__ int opaque(int v) {
 // next use (MachineSink ignores sched_barrier), which multiplies live registers in the unrolled solve.
 __device__ __forceinline__ void pin(float& v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ void pin(double& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(unsigned& v) { asm volatile("" : "+v"(v)); }
 
 __device__ __forceinline__ Task load_task(const Task* p) {
     Task t = *p;
@@ -283,6 +284,21 @@ __device__ __forceinline__ void split3(float x0, float x1, unsigned& h, unsigned
     l = pk_bf16(s0, s1);
 }
 __device__ __forceinline__ bf16x8 as_bf16x8(const u32x4& v) { return __builtin_bit_cast(bf16x8, v); }
+// One 32-entry block of a bf16 partial product: D += A^T B over k = 32 (lane (g, i) element e <-> entry 8g + e).
+__device__ __forceinline__ f32x4 mfma_k32(const u32x4& a, const u32x4& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b), c, 0, 0, 0);
+}
+// Close a group of v_mfma_f32_16x16x32_bf16: the compiler lets VALU instructions overwrite an MFMA's
+// A/B/C registers one instruction after it (it models the operands as read at issue), which on gfx950
+// intermittently corrupted the Gram (found as run-to-run differences in ~0.1% of rows, tools/determinism.py).
+// Every split step therefore issues its MFMAs as one group (sched_barrier before it) and ends it with 16
+// wait states before any later instruction may touch the operand registers: bitwise deterministic, same speed.
+#define MFMA_DRAIN()                                \
+    do {                                            \
+        __builtin_amdgcn_sched_barrier(0);          \
+        asm volatile("s_nop 7\n\ts_nop 7");         \
+        __builtin_amdgcn_sched_barrier(0);          \
+    } while (0)
 
 template <int C>
 struct MfmaAcc {
@@ -737,34 +753,43 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
 #pragma unroll
                     for (int b = 0; b < C; ++b)
 #pragma unroll
-                        for (int q = 0; q < 4; ++q)
-                            P[pl][b][q] = __builtin_amdgcn_perm(y[2 * q + 1].w[2 * pl + (b >> 1)],
-                                                                y[2 * q].w[2 * pl + (b >> 1)],
-                                                                (b & 1) ? 0x07060302u : 0x05040100u);
+                        for (int q = 0; q < 4; ++q) {
+                            unsigned v = __builtin_amdgcn_perm(y[2 * q + 1].w[2 * pl + (b >> 1)],
+                                                               y[2 * q].w[2 * pl + (b >> 1)],
+                                                               (b & 1) ? 0x07060302u : 0x05040100u);
+                            pin(v);
+                            P[pl][b][q] = v;
+                        }
                 u32x4 R;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) R[q] = pk_bf16(x.r[q >> 1][2 * (q & 1)], x.r[q >> 1][2 * (q & 1) + 1]);
+                for (int q = 0; q < 4; ++q) {
+                    unsigned v = pk_bf16(x.r[q >> 1][2 * (q & 1)], x.r[q >> 1][2 * (q & 1) + 1]);
+                    pin(v);
+                    R[q] = v;
+                }
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int b1 = 0; b1 < C; ++b1)
 #pragma unroll
                     for (int b2 = b1; b2 < C; ++b2) {
                         f32x4 t = acc.g[tile_index<C>(b1, b2)];
-                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[1][b1]), as_bf16x8(P[1][b2]), t, 0, 0, 0);
-                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[0][b1]), as_bf16x8(P[2][b2]), t, 0, 0, 0);
-                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[2][b1]), as_bf16x8(P[0][b2]), t, 0, 0, 0);
-                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[0][b1]), as_bf16x8(P[1][b2]), t, 0, 0, 0);
-                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[1][b1]), as_bf16x8(P[0][b2]), t, 0, 0, 0);
-                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[0][b1]), as_bf16x8(P[0][b2]), t, 0, 0, 0);
+                        t = mfma_k32(P[1][b1], P[1][b2], t);
+                        t = mfma_k32(P[0][b1], P[2][b2], t);
+                        t = mfma_k32(P[2][b1], P[0][b2], t);
+                        t = mfma_k32(P[0][b1], P[1][b2], t);
+                        t = mfma_k32(P[1][b1], P[0][b2], t);
+                        t = mfma_k32(P[0][b1], P[0][b2], t);
                         acc.g[tile_index<C>(b1, b2)] = t;
                     }
 #pragma unroll
                 for (int b = 0; b < C; ++b) {
                     f32x4 t = racc[b];
-                    t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[2][b]), as_bf16x8(R), t, 0, 0, 0);
-                    t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[1][b]), as_bf16x8(R), t, 0, 0, 0);
-                    t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(P[0][b]), as_bf16x8(R), t, 0, 0, 0);
+                    t = mfma_k32(P[2][b], R, t);
+                    t = mfma_k32(P[1][b], R, t);
+                    t = mfma_k32(P[0][b], R, t);
                     racc[b] = t;
                 }
+                MFMA_DRAIN();
             };
             if (nblk > 0) {
                 Cols I0, I1;
@@ -845,23 +870,30 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                     for (int q = 0; q < 4; ++q) {
                         unsigned h, m, l;
                         split3(y[2 * q][b], y[2 * q + 1][b], h, m, l);
+                        pin(h);
+                        pin(m);
+                        pin(l);
                         H[b][q] = h;
                         M[b][q] = m;
                         L[b][q] = l;
                     }
+                // the operands are materialised above (pin: MachineSink ignores sched_barrier), so the MFMA group
+                // below contains no VALU that could overwrite an operand register of an MFMA in flight
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int b1 = 0; b1 < C; ++b1)
 #pragma unroll
                     for (int b2 = b1; b2 < C; ++b2) {
                         f32x4 t = acc.g[tile_index<C>(b1, b2)];
-                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(M[b1]), as_bf16x8(M[b2]), t, 0, 0, 0);
-                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(H[b1]), as_bf16x8(L[b2]), t, 0, 0, 0);
-                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(L[b1]), as_bf16x8(H[b2]), t, 0, 0, 0);
-                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(H[b1]), as_bf16x8(M[b2]), t, 0, 0, 0);
-                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(M[b1]), as_bf16x8(H[b2]), t, 0, 0, 0);
-                        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(H[b1]), as_bf16x8(H[b2]), t, 0, 0, 0);
+                        t = mfma_k32(M[b1], M[b2], t);
+                        t = mfma_k32(H[b1], L[b2], t);
+                        t = mfma_k32(L[b1], H[b2], t);
+                        t = mfma_k32(H[b1], M[b2], t);
+                        t = mfma_k32(M[b1], H[b2], t);
+                        t = mfma_k32(H[b1], H[b2], t);
                         acc.g[tile_index<C>(b1, b2)] = t;
                     }
+                MFMA_DRAIN();
 #pragma unroll
                 for (int t = 0; t < B; ++t)
 #pragma unroll
