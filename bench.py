@@ -114,6 +114,10 @@ def main():
     ap.add_argument("--lam", type=float, default=0.05)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--overlap-chunks", type=int, default=4, help="user-half chunks per all-gather overlap (N > 1)")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="N > 1 ranks all on cuda:0 over gloo: rehearses the multi-rank driver on a one-GPU box "
+                         "(RCCL needs one GPU per rank); not a performance configuration")
     args = ap.parse_args()
 
     import numpy as np
@@ -127,9 +131,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"bench: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
+    if args.rehearse_one_gpu:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
 
     def barrier():
         if world > 1:
@@ -139,7 +148,7 @@ def main():
     ds = cfk.Dataset.synthetic_netflix(args.users, args.movies, args.nnz, args.seed, nthreads=min(16, os.cpu_count()))
     nm, nu, nnz = ds.counts()
     app = cfk.ALSApp(world, args.k, args.lam, args.steps, precision="f32", seed=42, device=local, rank=rank,
-                     world_size=world).setup(ds, check_duplicates=False)
+                     world_size=world, overlap_chunks=args.overlap_chunks).setup(ds, check_duplicates=False)
     t_setup = time.perf_counter() - t_setup
 
     for _ in range(args.warmup):
@@ -157,7 +166,7 @@ def main():
     elapsed = time.perf_counter() - t0
     app.engine.set_timing(False)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.rehearse_one_gpu else f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

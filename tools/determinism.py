@@ -3,7 +3,7 @@
 (with the user half run in between, which reuses the shared partial-slot workspace) must give identical
 factors. Variants are env settings applied at engine creation.
 
-  python tools/determinism.py [VAR=VAL[,VAR=VAL]] ...
+  [DET_K=128] python tools/determinism.py [VAR=VAL[,VAR=VAL]] ...
 """
 import os
 import sys
@@ -18,14 +18,15 @@ def main():
     import __graft_entry__
     cfk = __graft_entry__.load_package()
     ds = cfk.Dataset.synthetic_netflix(480_189, 17_770, 100_000_000, 0xA15, nthreads=16)
-    U0 = ds.init_user_factors(64, 42)
+    k = int(os.environ.get("DET_K", "64"))
+    U0 = ds.init_user_factors(k, 42)
     deg = np.diff(ds.shard_block(0)["row_ptr"])
     for v in (sys.argv[1:] or ["DEFAULT=1"]):
         saved = dict(os.environ)
         for kv in v.split(","):
             a, c = kv.split("=")
             os.environ[a] = c
-        eng = cfk.ALSEngine(64, "f32")
+        eng = cfk.ALSEngine(k, "f32")
         eng.use_torch_stream()
         for side in (0, 1):
             b = ds.shard_coo(side)
