@@ -48,6 +48,7 @@ _pi64 = ctypes.POINTER(ctypes.c_int64)
 _pi32 = ctypes.POINTER(ctypes.c_int32)
 _pi16 = ctypes.POINTER(ctypes.c_int16)
 _pf = ctypes.POINTER(ctypes.c_float)
+_pu8 = ctypes.POINTER(ctypes.c_uint8)
 _pd = ctypes.POINTER(ctypes.c_double)
 _ppv = ctypes.POINTER(ctypes.c_void_p)
 
@@ -92,6 +93,12 @@ SIGNATURES = [
     ("als_u01", _f, [_u64, _i64, ctypes.c_int32]),
     ("als_write_prediction_csv", _i, [ctypes.c_char_p, _pf, _i64, _i64, _pf, _i64, _i64, _i]),
     ("als_write_prediction_matrix_csv", _i, [ctypes.c_char_p, _pf, _i64, _i64]),
+    ("als_feature_message_size", _i64, [_i64, _i]),
+    ("als_feature_message_encode", _i, [ctypes.c_int32, _pi32, _i64, _pf, _i, _pu8, _i64, _pi64]),
+    ("als_feature_message_decode", _i, [_pu8, _i64, _i, _pi32, _pi32, _i64, _pi64, _pf]),
+    ("als_id_rating_encode", _i, [ctypes.c_int32, ctypes.c_int16, _pu8]),
+    ("als_id_rating_decode", _i, [_pu8, _i64, _pi32, _pi16]),
+    ("als_encode_feature_messages", _i, [_vp, _i, _i, _i, _pf, _i64, _pu8, _i64, _pi64, _pi64, _pi32, _pi64, _i64]),
 ]
 
 

@@ -153,6 +153,25 @@ class Dataset:
         call("als_dataset_slots", self._h, side, n_shards, ptr(out, ctypes.c_int64))
         return out
 
+    def feature_messages(self, side, n_partitions: int, factors: np.ndarray) -> tuple[bytes, np.ndarray, np.ndarray]:
+        """The out-block fan-out of one half as Kafka FeatureMessage records (MFeatureCalculator.java:122-131):
+        (concatenated payload, record keys = target partitions, byte offsets with a final end offset).
+        factors: one row per entity of `side` in ascending raw-id order."""
+        F = np.ascontiguousarray(factors, np.float32)
+        k = F.shape[1]
+        length = ctypes.c_int64()
+        n_msg = ctypes.c_int64()
+        call("als_encode_feature_messages", self._h, _side(side), n_partitions, k, None, k, None, 0,
+             ctypes.byref(length), ctypes.byref(n_msg), None, None, 0)
+        out = np.zeros(max(length.value, 1), np.uint8)
+        keys = np.zeros(n_msg.value, np.int32)
+        offs = np.zeros(n_msg.value + 1, np.int64)
+        call("als_encode_feature_messages", self._h, _side(side), n_partitions, k, ptr(F, ctypes.c_float), k,
+             ptr(out, ctypes.c_uint8), length.value, ctypes.byref(length), ctypes.byref(n_msg),
+             ptr(keys, ctypes.c_int32), ptr(offs, ctypes.c_int64), n_msg.value)
+        offs[-1] = length.value
+        return out[:length.value].tobytes(), keys, offs
+
     def init_user_factors(self, k: int, seed: int = 42, n_shards: int = 1, ld: int | None = None) -> np.ndarray:
         """U0 in slot order (UFeatureInitializer.java:50-56 with the shared seeded generator)."""
         ld = k if ld is None else ld
@@ -179,6 +198,46 @@ def write_prediction_matrix_csv(path: str, P: np.ndarray) -> None:
     """The collector's CSV from an already computed prediction matrix (e.g. ALSEngine.predict)."""
     P = np.ascontiguousarray(P, np.float32)
     call("als_write_prediction_matrix_csv", path.encode(), ptr(P, ctypes.c_float), P.shape[0], P.shape[1])
+
+
+def encode_feature_message(entity_id: int, deps, features) -> bytes:
+    """FeatureMessageSerializer (FeatureMessageSerializer.java:27-37): big-endian wire bytes."""
+    d = np.ascontiguousarray(deps if deps is not None else [], np.int32)
+    f = np.ascontiguousarray(features, np.float32)
+    n = _lib.lib().als_feature_message_size(d.size, f.size)
+    out = np.zeros(n, np.uint8)
+    call("als_feature_message_encode", entity_id, ptr(d, ctypes.c_int32), d.size, ptr(f, ctypes.c_float), f.size,
+         ptr(out, ctypes.c_uint8), n, None)
+    return out.tobytes()
+
+
+def decode_feature_message(data: bytes, num_features: int) -> tuple[int, np.ndarray, np.ndarray]:
+    """FeatureMessageDeserializer (FeatureMessageDeserializer.java:30-56) -> (id, dependent ids, features)."""
+    buf = np.frombuffer(data, np.uint8).copy()
+    eid = ctypes.c_int32()
+    nd = ctypes.c_int64()
+    call("als_feature_message_decode", ptr(buf, ctypes.c_uint8), buf.size, num_features, ctypes.byref(eid), None, 0,
+         ctypes.byref(nd), None)
+    deps = np.zeros(nd.value, np.int32)
+    f = np.zeros(num_features, np.float32)
+    call("als_feature_message_decode", ptr(buf, ctypes.c_uint8), buf.size, num_features, None,
+         ptr(deps, ctypes.c_int32), nd.value, None, ptr(f, ctypes.c_float))
+    return eid.value, deps, f
+
+
+def encode_id_rating(entity_id: int, rating: int) -> bytes:
+    """IdRatingPairMessageSerializer (IdRatingPairMessageSerializer.java:24-33): 6 big-endian bytes."""
+    out = np.zeros(6, np.uint8)
+    call("als_id_rating_encode", entity_id, rating, ptr(out, ctypes.c_uint8))
+    return out.tobytes()
+
+
+def decode_id_rating(data: bytes) -> tuple[int, int]:
+    buf = np.frombuffer(data, np.uint8).copy()
+    eid = ctypes.c_int32()
+    r = ctypes.c_int16()
+    call("als_id_rating_decode", ptr(buf, ctypes.c_uint8), buf.size, ctypes.byref(eid), ctypes.byref(r))
+    return eid.value, r.value
 
 
 class ALSEngine:

@@ -90,6 +90,31 @@ int als_write_prediction_csv(const char* path, const float* U, int64_t n_users, 
  * n_users x n_movies. */
 int als_write_prediction_matrix_csv(const char* path, const float* P, int64_t n_users, int64_t n_movies);
 
+/* ---- Kafka wire formats (big-endian, as the reference's serializers write them) ----
+ * FeatureMessage = i32 id | i32 n_deps | n_deps x i32 dependent id | i32 num_features | num_features x f32
+ *   (FeatureMessageSerializer.java:27-37, ListSerializer.java:72-84, FloatArraySerializer.java:15-24;
+ *   NaN written as Float.floatToIntBits' canonical 0x7fc00000). Size = 12 + 4 n_deps + 4 num_features. */
+int64_t als_feature_message_size(int64_t n_deps, int num_features);
+/* *length = the message size (also when the buffer is too small). */
+int als_feature_message_encode(int32_t id, const int32_t* deps, int64_t n_deps, const float* features,
+                               int num_features, uint8_t* out, int64_t capacity, int64_t* length);
+/* FeatureMessageDeserializer.java:30-56: the dependent-id count is inferred from `length` and num_features
+ * (= ALSApp.NUM_FEATURES); inconsistent lengths or counts are ALS_ERR_PARSE. deps may be NULL (count only). */
+int als_feature_message_decode(const uint8_t* data, int64_t length, int num_features, int32_t* id, int32_t* deps,
+                               int64_t deps_capacity, int64_t* n_deps, float* features);
+/* IdRatingPairMessage = i32 id | i16 rating, 6 bytes (IdRatingPairMessageSerializer.java:24-33). */
+int als_id_rating_encode(int32_t id, int16_t rating, uint8_t* out6);
+int als_id_rating_decode(const uint8_t* data, int64_t length, int32_t* id, int16_t* rating);
+/* The out-block fan-out of one half (MFeatureCalculator.java:122-131, UFeatureCalculator.java:124-128,
+ * UFeatureInitializer.java:61-64): for every entity of `side` in ascending raw id, one FeatureMessage per
+ * partition of its out-block (partitions in first-appearance order over its in-block), carrying the in-block
+ * ids with id % n_partitions == partition in arrival order; keys[m] = that partition (the record key).
+ * factors: row i = the i-th entity in ascending raw-id order, stride ld floats. out == NULL: size query
+ * (*length bytes, *n_messages messages). offsets[m] = byte offset of message m in out. */
+int als_encode_feature_messages(const als_dataset* ds, int side, int n_partitions, int num_features,
+                                const float* factors, int64_t ld, uint8_t* out, int64_t capacity, int64_t* length,
+                                int64_t* n_messages, int32_t* keys, int64_t* offsets, int64_t messages_capacity);
+
 #ifdef __cplusplus
 }
 #endif

@@ -15,7 +15,7 @@ def _declared_symbols():
     names = []
     for h in ("als.h", "als_host.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
-        names += re.findall(r"^\s*(?:int|float|const char\*)\s+(als_\w+)\s*\(", src, flags=re.M)
+        names += re.findall(r"^\s*(?:int|int64_t|float|const char\*)\s+(als_\w+)\s*\(", src, flags=re.M)
     return names
 
 
