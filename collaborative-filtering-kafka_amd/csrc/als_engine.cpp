@@ -86,6 +86,8 @@ struct als_engine {
     size_t partial_bytes = 0;
     void* d_split = nullptr;        // pre-split opposite table (cfk::launch_presplit), sized for the larger need
     size_t split_bytes = 0;
+    void* h_stage = nullptr;        // pinned staging of als_write_factors (cfk::launch_upload)
+    size_t stage_bytes = 0;
     int min_waves = 0;              // ALS_MFMA_WAVES override of the per-block occupancy choice (0 = auto)
     int32_t debug_flags = 0;        // ALS_DEBUG_SKIP_SOLVE=1 -> cfk::SOLVE_FLAG_SKIP_SOLVE (tools/kbench.py only)
     bool timing = false;
@@ -193,6 +195,7 @@ int als_engine_destroy(als_engine* e) {
         if (f.owned) (void)hipFree(f.ptr);
     (void)hipFree(e->d_partials);
     (void)hipFree(e->d_split);
+    (void)hipHostFree(e->h_stage);
     for (auto& rec : e->pending)
         for (auto ev : rec.ev) (void)hipEventDestroy(ev);
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
@@ -487,11 +490,27 @@ int als_write_factors(als_engine* e, int side, int64_t row0, int64_t n_rows, con
     if (!host_src) return fail(ALS_ERR_INVALID_ARGUMENT, "host_src is NULL");
     HIP_TRY(hipSetDevice(e->device));
     const size_t es = e->elem();
-    // dst pitch = kp, width = k elements; the padding columns are zeroed first.
-    char* dst = (char*)f.ptr + (size_t)row0 * e->kp * es;
-    HIP_TRY(hipMemsetAsync(dst, 0, (size_t)n_rows * e->kp * es, e->stream));
-    HIP_TRY(hipMemcpy2DAsync(dst, e->kp * es, host_src, src_ld * es, e->k * es, n_rows, hipMemcpyHostToDevice, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    // Rows are packed kp wide (padding columns zero) into pinned staging and written by a copy kernel
+    // (cfk::launch_upload), never by SDMA: see the note at upload16 in als_kernels.hip.
+    const size_t row_bytes = (size_t)e->kp * es;
+    constexpr size_t STAGE = 32u << 20;
+    if (!e->h_stage) {
+        HIP_TRY(hipHostMalloc(&e->h_stage, STAGE, hipHostMallocDefault));
+        e->stage_bytes = STAGE;
+    }
+    const int64_t rows_per = (int64_t)(e->stage_bytes / row_bytes);
+    for (int64_t r = 0; r < n_rows; r += rows_per) {
+        const int64_t nr = std::min(rows_per, n_rows - r);
+        char* stage = (char*)e->h_stage;
+        const char* src = (const char*)host_src + (size_t)r * src_ld * es;
+        for (int64_t i = 0; i < nr; ++i) {
+            std::memcpy(stage + i * row_bytes, src + (size_t)i * src_ld * es, (size_t)e->k * es);
+            std::memset(stage + i * row_bytes + (size_t)e->k * es, 0, row_bytes - (size_t)e->k * es);
+        }
+        HIP_TRY(cfk::launch_upload(stage, (char*)f.ptr + (size_t)(row0 + r) * row_bytes, (size_t)nr * row_bytes,
+                                   e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));   // the staging buffer is reused by the next chunk
+    }
     return ALS_OK;
 }
 

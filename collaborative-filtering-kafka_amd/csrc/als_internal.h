@@ -88,6 +88,8 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
 // h(f0,f1) h(f2,f3) m(f0,f1) m(f2,f3) l(f0,f1) l(f2,f3).
 constexpr int PRESPLIT_ROW_BYTES = 384;
 hipError_t launch_presplit(const float* src, void* dst, int64_t n_rows, hipStream_t s);
+// bytes % 16 == 0; host_pinned must stay valid until the stream has passed the copy
+hipError_t launch_upload(const void* host_pinned, void* dst, size_t bytes, hipStream_t s);
 // out[u][m] = Java-float dot of U row urows[u] and M row mrows[m] (device arrays; out row-major n_u x n_m).
 hipError_t launch_predict(int precision, const void* U, const void* M, int kp, int k, const int64_t* urows,
                           int64_t n_u, const int64_t* mrows, int64_t n_m, float* out, hipStream_t s);

@@ -293,12 +293,20 @@ __device__ __forceinline__ f32x4 mfma_k32(const u32x4& a, const u32x4& b, f32x4 
 // intermittently corrupted the Gram (found as run-to-run differences in ~0.1% of rows, tools/determinism.py).
 // Every split step therefore issues its MFMAs as one group (sched_barrier before it) and ends it with 16
 // wait states before any later instruction may touch the operand registers: bitwise deterministic, same speed.
-#define MFMA_DRAIN()                                \
-    do {                                            \
-        __builtin_amdgcn_sched_barrier(0);          \
-        asm volatile("s_nop 7\n\ts_nop 7");         \
-        __builtin_amdgcn_sched_barrier(0);          \
+#ifndef CFK_DRAIN_NOPS
+#define CFK_DRAIN_NOPS 2
+#endif
+#define MFMA_DRAIN()                                                          \
+    do {                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                    \
+        static_for<0, CFK_DRAIN_NOPS>([&](auto) { asm volatile("s_nop 7"); }); \
+        __builtin_amdgcn_sched_barrier(0);                                    \
     } while (0)
+// The solve's v_mfma_f32_16x16x4_f32 groups get the same treatment when CFK_SOLVE_DRAIN is set.
+#ifndef CFK_SOLVE_DRAIN
+#define CFK_SOLVE_DRAIN 0
+#endif
+__device__ __forceinline__ void pin4(f32x4& v) { asm volatile("" : "+v"(v)); }
 
 template <int C>
 struct MfmaAcc {
@@ -310,6 +318,47 @@ struct MfmaAcc {
 
 template <int C>
 __host__ __device__ constexpr int tile_index(int b1, int b2) { return b1 * C - (b1 * (b1 - 1)) / 2 + (b2 - b1); }
+
+// Diagonal tiles of the split Gram: hm + mh = X + X^T and hl + lh = Y + Y^T with X = h m^T, Y = h l^T, so the
+// split paths accumulate X + Y per diagonal tile in E (2 MFMAs instead of 4 per block) and fold
+// G_bb += E_b + E_b^T once per task: 8 of the 60 Gram MFMAs per block saved.
+#ifndef CFK_DIAG_SYM
+#define CFK_DIAG_SYM 1
+#endif
+
+// G_bb += E_b + E_b^T. E^T via v_mfma_f32_16x16x4_f32 against the identity: with both operands in accumulator
+// layout the four k-slices compute D += E^T I (see solve_tiles), each output one exact product plus C.
+template <int C>
+__device__ __forceinline__ void fold_diag(MfmaAcc<C>& acc, f32x4 (&E)[C], int lane) {
+    f32x4 I;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float v = ((lane >> 4) * 4 + r == (lane & 15)) ? 1.f : 0.f;
+        pin(v);
+        I[r] = v;
+    }
+    f32x4 D[C];
+#pragma unroll
+    for (int b = 0; b < C; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v = acc.g[tile_index<C>(b, b)][r] + E[b][r];
+            float e = E[b][r];
+            pin(v);
+            pin(e);
+            D[b][r] = v;
+            E[b][r] = e;
+        }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int b = 0; b < C; ++b) {
+        f32x4 t = D[b];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) t = __builtin_amdgcn_mfma_f32_16x16x4f32(E[b][s], I[s], t, 0, 0, 0);
+        acc.g[tile_index<C>(b, b)] = t;
+    }
+    MFMA_DRAIN();
+}
 
 // ---------------------------------------------------------------------------------------------------
 // Cross-lane moves on the 4 x 16 lane grid (row g = lane >> 4, column c = lane & 15), VALU-only (no LDS)
@@ -484,16 +533,29 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
         // receives the same single update per P as in any order: bitwise equal.
         static_for<0, C - 1 - P>([&](auto Q_) {
             constexpr int J = C - 1 - decltype(Q_)::value;
-            const f32x4 TPJ = T.get(tile_index<C>(P, J));
+            f32x4 TPJ = T.get(tile_index<C>(P, J));
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (CFK_SOLVE_DRAIN) {
+                pin4(S);
+                pin4(TPJ);
+                pin4(v);
+                __builtin_amdgcn_sched_barrier(0);
+            }
 #pragma unroll
             for (int s = 0; s < 4; ++s) v = __builtin_amdgcn_mfma_f32_16x16x4f32(S[s], TPJ[s], v, 0, 0, 0);
+            if constexpr (CFK_SOLVE_DRAIN) MFMA_DRAIN();
             static_for<P + 1, J + 1>([&](auto I_) {
                 constexpr int I = decltype(I_)::value;
-                const f32x4 TPI = T.get(tile_index<C>(P, I));
+                f32x4 TPI = T.get(tile_index<C>(P, I));
                 f32x4 D = T.get(tile_index<C>(I, J));
+                if constexpr (CFK_SOLVE_DRAIN) {
+                    pin4(TPI);
+                    pin4(D);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
 #pragma unroll
                 for (int s = 0; s < 4; ++s) D = __builtin_amdgcn_mfma_f32_16x16x4f32(TPI[s], v[s], D, 0, 0, 0);
+                if constexpr (CFK_SOLVE_DRAIN) MFMA_DRAIN();
                 T.put(tile_index<C>(I, J), D);
             });
             T.put(tile_index<C>(P, J), v);   // block row P now holds V'_PJ
@@ -656,6 +718,9 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
     for (int p = 0; p < Acc::NT; ++p) acc.g[p] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < C; ++c) acc.rhs[c] = 0.f;
+    f32x4 E[C];   // split paths: h m^T + h l^T of the diagonal tiles (fold_diag)
+#pragma unroll
+    for (int c = 0; c < C; ++c) E[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     float* part = (float*)a.partials;
     if (tk.kind == TASK_REDUCE) {
@@ -774,10 +839,17 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                     for (int b2 = b1; b2 < C; ++b2) {
                         f32x4 t = acc.g[tile_index<C>(b1, b2)];
                         t = mfma_k32(P[1][b1], P[1][b2], t);
-                        t = mfma_k32(P[0][b1], P[2][b2], t);
-                        t = mfma_k32(P[2][b1], P[0][b2], t);
-                        t = mfma_k32(P[0][b1], P[1][b2], t);
-                        t = mfma_k32(P[1][b1], P[0][b2], t);
+                        if (CFK_DIAG_SYM && b1 == b2) {
+                            f32x4 e = E[b1];
+                            e = mfma_k32(P[0][b1], P[2][b1], e);
+                            e = mfma_k32(P[0][b1], P[1][b1], e);
+                            E[b1] = e;
+                        } else {
+                            t = mfma_k32(P[0][b1], P[2][b2], t);
+                            t = mfma_k32(P[2][b1], P[0][b2], t);
+                            t = mfma_k32(P[0][b1], P[1][b2], t);
+                            t = mfma_k32(P[1][b1], P[0][b2], t);
+                        }
                         t = mfma_k32(P[0][b1], P[0][b2], t);
                         acc.g[tile_index<C>(b1, b2)] = t;
                     }
@@ -886,10 +958,17 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                     for (int b2 = b1; b2 < C; ++b2) {
                         f32x4 t = acc.g[tile_index<C>(b1, b2)];
                         t = mfma_k32(M[b1], M[b2], t);
-                        t = mfma_k32(H[b1], L[b2], t);
-                        t = mfma_k32(L[b1], H[b2], t);
-                        t = mfma_k32(H[b1], M[b2], t);
-                        t = mfma_k32(M[b1], H[b2], t);
+                        if (CFK_DIAG_SYM && b1 == b2) {
+                            f32x4 e = E[b1];
+                            e = mfma_k32(H[b1], L[b1], e);
+                            e = mfma_k32(H[b1], M[b1], e);
+                            E[b1] = e;
+                        } else {
+                            t = mfma_k32(H[b1], L[b2], t);
+                            t = mfma_k32(L[b1], H[b2], t);
+                            t = mfma_k32(H[b1], M[b2], t);
+                            t = mfma_k32(M[b1], H[b2], t);
+                        }
                         t = mfma_k32(H[b1], H[b2], t);
                         acc.g[tile_index<C>(b1, b2)] = t;
                     }
@@ -1033,6 +1112,10 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             for (int t = 0; t < B; ++t)
                 if (t < last) mfma_step(y_c[t], x_c.r[t >> 2][t & 3]);   // wave-uniform
         }
+    }
+
+    if constexpr (SPLIT && CFK_DIAG_SYM) {
+        if (tk.kind != TASK_REDUCE) fold_diag<C>(acc, E, lane);
     }
 
     if (tk.kind == TASK_PARTIAL) {
@@ -1290,6 +1373,25 @@ hipError_t launch_predict(int precision, const void* U, const void* M, int kp, i
     else
         als_predict_kernel<double><<<grid, 256, 0, s>>>((const double*)U, (const double*)M, kp, k, urows, n_u, mrows, n_m,
                                                         out);
+    return hipGetLastError();
+}
+
+// Host -> device upload as a KERNEL write: each lane reads 16 B of pinned host memory (zero-copy, non-temporal)
+// and stores it to device memory through L2 -- the same coherence path as the solve kernels' own writes. Used
+// for factor tables: an SDMA copy over memory that kernels wrote (and may still hold in an XCD's L2) was
+// observed to leave stale rows for the next solve (tests/test_gpu_parity.py::test_bitwise_determinism...).
+__global__ __launch_bounds__(256) void upload16(const u32x4* __restrict__ src, u32x4* __restrict__ dst, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        dst[i] = __builtin_nontemporal_load(src + i);
+}
+
+hipError_t launch_upload(const void* host_pinned, void* dst, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    if (bytes % 16 != 0) return hipErrorInvalidValue;
+    const int64_t n = (int64_t)(bytes / 16);
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+    upload16<<<(unsigned)blocks, 256, 0, s>>>((const u32x4*)host_pinned, (u32x4*)dst, n);
     return hipGetLastError();
 }
 

@@ -3,7 +3,7 @@
 (with the user half run in between, which reuses the shared partial-slot workspace) must give identical
 factors. Variants are env settings applied at engine creation.
 
-  [DET_K=128] python tools/determinism.py [VAR=VAL[,VAR=VAL]] ...
+  [DET_K=128] [DET_REPS=3] python tools/determinism.py [VAR=VAL[,VAR=VAL]] ...
 """
 import os
 import sys
@@ -35,15 +35,34 @@ def main():
         os.environ.clear()
         os.environ.update(saved)
         Ms = []
-        for rep in range(3):
+        reps = int(os.environ.get("DET_REPS", "3"))
+        for rep in range(reps):
             eng.write_factors(1, U0)
             eng.solve_half(0, 0.05)
             Ms.append(eng.read_factors(0))
-            if rep == 1:
+            if rep == 1 or os.environ.get("DET_USER_EVERY_REP"):
                 eng.solve_half(1, 0.05)      # the user half overwrites the shared partial slots
-        for r in (1, 2):
+        blk0 = ds.shard_block(0)
+
+        def fp64_err(i, x):
+            # fp64 restatement of the movie update for row i (MFeatureCalculator.java:82-99) from U0
+            cols = blk0["col"][blk0["row_ptr"][i]:blk0["row_ptr"][i + 1]]
+            Y = U0[cols, :k].astype(np.float64)
+            r = blk0["ratings"][blk0["row_ptr"][i]:blk0["row_ptr"][i + 1]].astype(np.float64)
+            A = Y.T @ Y + np.float64(np.float32(0.05)) * len(cols) * np.eye(k)
+            ref = np.linalg.solve(A, Y.T @ r)
+            return float(np.max(np.abs(x[:k] - ref)) / np.max(np.abs(ref)))
+
+        for r in range(1, reps):
+            bad = np.nonzero(np.any(Ms[0] != Ms[r], axis=1))[0][:4]
+            if len(bad):
+                print(f"  vs fp64: rep0 {[fp64_err(i, Ms[0][i]) for i in bad]} rep{r} {[fp64_err(i, Ms[r][i]) for i in bad]}",
+                      flush=True)
             rows = np.nonzero(np.any(Ms[0] != Ms[r], axis=1))[0]
-            print(f"{v}: movie rep0 vs rep{r}: {len(rows)} differing rows; degrees {deg[rows][:12].tolist()}; "
+            rel = [float(np.max(np.abs(Ms[0][i] - Ms[r][i])) / max(float(np.max(np.abs(Ms[0][i]))), 1e-30))
+                   for i in rows[:12]]
+            print(f"{v}: movie rep0 vs rep{r}: {len(rows)} differing rows {rows[:12].tolist()} rel {rel}; "
+                  f"degrees {deg[rows][:12].tolist()}; "
                   f"stats {eng.block_stats(0)}", flush=True)
         eng.close()
 
