@@ -365,6 +365,23 @@ def test_bitwise_determinism_netflix_shape(cfk):
         eng.solve_half(1, LAM)
         Us.append(eng.read_factors(1))
     eng.close()
-    for r in (1, 2):
-        assert np.array_equal(Ms[0], Ms[r]), int(np.any(Ms[0] != Ms[r], axis=1).sum())
-        assert np.array_equal(Us[0], Us[r]), int(np.any(Us[0] != Us[r], axis=1).sum())
+    report = []
+    for name, reps in (("movie", Ms), ("user", Us)):
+        side = 0 if name == "movie" else 1
+        rows = sorted(set(np.nonzero(np.any(reps[0] != reps[1], axis=1))[0].tolist())
+                      | set(np.nonzero(np.any(reps[0] != reps[2], axis=1))[0].tolist()))
+        if not rows:
+            continue
+        blk = ds.shard_block(side)
+        opp = U0 if side == 0 else None
+        for i in rows[:4]:
+            lo, hi = int(blk["row_ptr"][i]), int(blk["row_ptr"][i + 1])
+            odd = [r for r in range(3) if sum(np.array_equal(reps[r][i], reps[q][i]) for q in range(3)) == 1]
+            err = []
+            if opp is not None:   # fp64 restatement of the movie update from U0 (MFeatureCalculator.java:82-99)
+                Y = opp[blk["col"][lo:hi], :64].astype(np.float64)
+                rr = blk["ratings"][lo:hi].astype(np.float64)
+                ref = np.linalg.solve(Y.T @ Y + np.float64(np.float32(LAM)) * (hi - lo) * np.eye(64), Y.T @ rr)
+                err = [float(np.max(np.abs(reps[r][i] - ref)) / np.max(np.abs(ref))) for r in range(3)]
+            report.append(f"{name} row {i} deg {hi - lo} deviating rep(s) {odd} fp64 err per rep {err}")
+    assert not report, f"{len(report)} nondeterministic rows: " + "; ".join(report)
