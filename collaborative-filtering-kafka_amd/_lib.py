@@ -58,6 +58,7 @@ SIGNATURES = [
     ("als_engine_create", _i, [_i, _i, _i, _ppv]),
     ("als_engine_destroy", _i, [_vp]),
     ("als_engine_set_stream", _i, [_vp, _vp]),
+    ("als_engine_use_default_stream", _i, [_vp]),
     ("als_factor_stride", _i, [_vp]),
     ("als_set_block", _i, [_vp, _i, _i64, _i64, _i64, _pi64, _pi32, _pi16]),
     ("als_set_block_coo", _i, [_vp, _i, _i64, _i64, _i64, _i64, _pi32, _pi32, _pi16]),

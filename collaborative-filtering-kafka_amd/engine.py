@@ -270,7 +270,13 @@ class ALSEngine:
 
     def use_torch_stream(self, stream: torch.cuda.Stream | None = None):
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        call("als_engine_set_stream", self._h, ctypes.c_void_p(s.cuda_stream))
+        if s.cuda_stream == 0:
+            # torch's default stream is the NULL stream: launch there too (a NULL handle passed to
+            # als_engine_set_stream would select a private non-blocking stream, unordered with torch's work
+            # and with the RCCL collectives that wait on torch's current stream)
+            call("als_engine_use_default_stream", self._h)
+        else:
+            call("als_engine_set_stream", self._h, ctypes.c_void_p(s.cuda_stream))
 
     def set_block(self, side, row_ptr, col, ratings, row_offset: int, n_opp_rows: int):
         rp = np.ascontiguousarray(row_ptr, np.int64)

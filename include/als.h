@@ -61,6 +61,10 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
 int als_engine_destroy(als_engine* e);
 /* Launch on a caller-provided hipStream_t (e.g. torch's current stream); NULL = engine-owned stream. */
 int als_engine_set_stream(als_engine* e, void* hip_stream);
+/* Launch on the device's NULL (legacy default) stream: the stream torch launches on when no other stream is
+ * current (its handle is 0, which als_engine_set_stream would read as "engine-owned"). The engine's kernels are
+ * then ordered with torch's work and with RCCL collectives issued against that stream. */
+int als_engine_use_default_stream(als_engine* e);
 int als_factor_stride(const als_engine* e);
 
 /* ---- in-block upload (constant over all iterations, README.md:146-147) ---------------------------- */
