@@ -385,3 +385,27 @@ def test_bitwise_determinism_netflix_shape(cfk):
                 err = [float(np.max(np.abs(reps[r][i] - ref)) / np.max(np.abs(ref))) for r in range(3)]
             report.append(f"{name} row {i} deg {hi - lo} deviating rep(s) {odd} fp64 err per rep {err}")
     assert not report, f"{len(report)} nondeterministic rows: " + "; ".join(report)
+
+
+def test_engine_ordered_with_torch_default_stream(cfk):
+    """use_torch_stream() on torch's default stream (handle 0) must put the engine on that NULL stream, so a torch
+    op (or an RCCL collective, which waits on torch's current stream) issued right after als_solve_half sees the
+    solved rows. The engine used to pick a private non-blocking stream here, and the all-gather of the multi-GPU
+    driver was then unordered with the solve."""
+    assert torch.cuda.current_stream().cuda_stream == 0
+    ds = cfk.Dataset.synthetic_netflix(200_000, 6_000, 20_000_000, 7, nthreads=16)
+    eng = cfk.ALSEngine(64, "f32")
+    eng.use_torch_stream()
+    for side in (0, 1):
+        b = ds.shard_coo(side)
+        eng.alloc_factors(side, b["n_slots"])
+        eng.set_block_coo(side, b["n_rows"], b["rows"], b["cols"], b["ratings"], 0, ds.shard_info(1 - side)["n_slots"])
+    eng.write_factors(1, ds.init_user_factors(64, 42))
+    torch.cuda.synchronize()
+    eng.solve_half(0, LAM)                                   # async on the engine's stream
+    seen = eng.factors[0][:-1, :64].clone().cpu().numpy()   # torch, default stream, issued immediately
+    torch.cuda.synchronize()
+    M = eng.read_factors(0)
+    eng.close()
+    assert np.abs(M).sum() > 0
+    assert np.array_equal(seen, M), int(np.any(seen != M, axis=1).sum())
