@@ -432,7 +432,7 @@ __device__ __forceinline__ void sweep_tile(f32x4& a, int lane) {
 // of each block; buf is KP floats of per-wave LDS.
 // Tile storage of the solve. Up to KP = 64 the tiles stay in the MFMA accumulator registers (RegTiles);
 // at KP = 128 (36 tiles = 144 registers per copy; the solve's VALU work needs them in the 256 architected
-// VGPRs) the working tiles and the kept copy live in per-wave LDS ([tile][reg][lane]: conflict-free b32
+// VGPRs) the working tiles live in per-wave LDS ([tile][lane][reg], CFK_LDS_B128; or [tile][reg][lane]: conflict-free b32
 // accesses) and are loaded a tile at a time (LdsTiles).
 template <int C>
 struct RegTiles {
@@ -446,15 +446,26 @@ struct RegStore {
     __device__ __forceinline__ f32x4 get(int i) const { return t[i]; }
     __device__ __forceinline__ void put(int i, const f32x4& v) { t[i] = v; }
 };
+// KP = 128 working tiles: [tile][lane][reg] so a tile moves with one ds_read_b128 / ds_write_b128 per lane
+// (kbench, k = 128: user half 23.3 -> 20.5 ms against the [tile][reg][lane] b32 layout, at the cost of 3 VGPR
+// spills); CFK_LDS_B128=0 restores the b32 layout
+#ifndef CFK_LDS_B128
+#define CFK_LDS_B128 1
+#endif
 struct LdsTiles {
-    float* p;   // per-wave base + lane
+    float* p;   // per-wave base + lane (b32 layout [tile][reg][lane]) or + 4 * lane (b128 layout [tile][lane][reg])
     __device__ __forceinline__ f32x4 get(int i) const {
+        if constexpr (CFK_LDS_B128) return *(const f32x4*)(p + i * 256);
         f32x4 v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = p[(i * 4 + r) * 64];
         return v;
     }
     __device__ __forceinline__ void put(int i, const f32x4& v) {
+        if constexpr (CFK_LDS_B128) {
+            *(f32x4*)(p + i * 256) = v;
+            return;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) p[(i * 4 + r) * 64] = v[r];
     }
@@ -1138,7 +1149,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
         return;
     }
     if constexpr (tiles_in_lds<C>()) {
-        LdsTiles T{tiles_lds[wave] + lane};
+        LdsTiles T{tiles_lds[wave] + (CFK_LDS_B128 ? 4 : 1) * lane};
         RegStore<C> A0;
 #pragma unroll
         for (int p = 0; p < Acc::NT; ++p) T.put(p, acc.g[p]);
