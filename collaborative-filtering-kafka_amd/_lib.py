@@ -26,7 +26,7 @@ F64 = 1
 
 _STATUS = {
     1: "ALS_ERR_INVALID_ARGUMENT", 2: "ALS_ERR_UNSUPPORTED", 3: "ALS_ERR_DEVICE", 4: "ALS_ERR_OUT_OF_MEMORY",
-    5: "ALS_ERR_STATE", 6: "ALS_ERR_IO", 7: "ALS_ERR_PARSE", 8: "ALS_ERR_DATA",
+    5: "ALS_ERR_STATE", 6: "ALS_ERR_IO", 7: "ALS_ERR_PARSE", 8: "ALS_ERR_DATA", 9: "ALS_ERR_INTEGRITY",
 }
 
 
@@ -73,8 +73,10 @@ SIGNATURES = [
     ("als_predict", _i, [_vp, _pi64, _i64, _pi64, _i64, _pf]),
     ("als_sq_error", _i, [_vp, _i, _pd, _pi64]),
     ("als_synchronize", _i, [_vp]),
+    ("als_integrity_status", _i, [_vp, ctypes.POINTER(ctypes.c_uint32), _i]),
     ("als_set_timing", _i, [_vp, _i]),
     ("als_timing_collect", _i, [_vp, _i, _pd, _pd, _pi64]),
+    ("als_debug_copy_partials", _i, [_vp, _vp, _i64, _pi64]),
     ("als_block_stats", _i, [_vp, _i, _pi64, _pi64, _pi64]),
     # als_host.h
     ("als_dataset_load_netflix", _i, [ctypes.c_char_p, _ppv]),

@@ -86,10 +86,16 @@ struct als_engine {
     size_t partial_bytes = 0;
     void* d_split = nullptr;        // pre-split opposite table (cfk::launch_presplit), sized for the larger need
     size_t split_bytes = 0;
-    void* h_stage = nullptr;        // pinned staging of als_write_factors (cfk::launch_upload)
+    void* h_stage = nullptr;        // pinned staging of als_write_factors / als_read_factors (copy kernels)
     size_t stage_bytes = 0;
+    uint32_t* d_integrity = nullptr;   // cfk::INTEGRITY_WORDS: partial slots that failed their check
+    uint32_t gen = 0;               // launch generation of the next PARTIAL/REDUCE pair
     int min_waves = 0;              // ALS_MFMA_WAVES override of the per-block occupancy choice (0 = auto)
     int32_t debug_flags = 0;        // ALS_DEBUG_SKIP_SOLVE=1 -> cfk::SOLVE_FLAG_SKIP_SOLVE (tools/kbench.py only)
+    uint32_t debug_gen_skew = 0;    // ALS_DEBUG_REDUCE_GEN_SKEW=n: REDUCE decodes with generation + n (tests the
+                                    // integrity check: every slot then reads as written by another launch)
+    bool debug_fixed_gen = false;   // ALS_DEBUG_FIXED_GEN=1: every launch uses generation 1, so partial slots of
+                                    // repeated launches are bitwise comparable (als_debug_copy_partials)
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     std::vector<TimingRec> pending;
@@ -100,6 +106,21 @@ namespace {
 
 int check_engine(const als_engine* e) {
     if (!e) return fail(ALS_ERR_INVALID_ARGUMENT, "engine is NULL");
+    return ALS_OK;
+}
+
+// Drain the engine's stream and read the partial-slot integrity record (cfk::SlotCodec): a REDUCE task that
+// found a slot it could not see freshly written by this launch's PARTIAL task makes every later synchronising
+// call fail until als_integrity_status(..., reset = 1).
+int sync_checked(als_engine* e) {
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    uint32_t rec[cfk::INTEGRITY_WORDS];
+    HIP_TRY(hipMemcpy(rec, e->d_integrity, sizeof(rec), hipMemcpyDeviceToHost));
+    if (rec[0] != 0)
+        return fail(ALS_ERR_INTEGRITY,
+                    "%u REDUCE tasks found partial slots that failed their check (first: launch generation %u, slot "
+                    "%u, row %u): partial sums its PARTIAL task's writes had not reached",
+                    rec[0], rec[1], rec[2], rec[3]);
     return ALS_OK;
 }
 int check_side(int side) {
@@ -177,6 +198,8 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
     if (const char* env = getenv("ALS_MFMA_WAVES")) e->min_waves = std::max(0, atoi(env));
     if (const char* env = getenv("ALS_DEBUG_SKIP_SOLVE"))
         if (env[0] == '1') e->debug_flags |= cfk::SOLVE_FLAG_SKIP_SOLVE;
+    if (const char* env = getenv("ALS_DEBUG_REDUCE_GEN_SKEW")) e->debug_gen_skew = (uint32_t)atoi(env);
+    if (const char* env = getenv("ALS_DEBUG_FIXED_GEN")) e->debug_fixed_gen = env[0] == '1';
     if (const char* env = getenv("ALS_DEBUG_SKIP_REFINE"))
         if (env[0] == '1') e->debug_flags |= cfk::SOLVE_FLAG_SKIP_REFINE;
     hipError_t st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
@@ -185,6 +208,14 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
         return fail(ALS_ERR_DEVICE, "hipStreamCreate: %s", hipGetErrorString(st));
     }
     e->own_stream = true;
+    st = hipMalloc((void**)&e->d_integrity, cfk::INTEGRITY_WORDS * sizeof(uint32_t));
+    if (st == hipSuccess) st = hipMemset(e->d_integrity, 0, cfk::INTEGRITY_WORDS * sizeof(uint32_t));
+    if (st != hipSuccess) {
+        (void)hipStreamDestroy(e->stream);
+        (void)hipFree(e->d_integrity);
+        delete e;
+        return fail(ALS_ERR_DEVICE, "integrity record: %s", hipGetErrorString(st));
+    }
     *out = e;
     return ALS_OK;
 }
@@ -199,6 +230,7 @@ int als_engine_destroy(als_engine* e) {
     (void)hipFree(e->d_partials);
     (void)hipFree(e->d_split);
     (void)hipHostFree(e->h_stage);
+    (void)hipFree(e->d_integrity);
     for (auto& rec : e->pending)
         for (auto ev : rec.ev) (void)hipEventDestroy(ev);
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
@@ -243,6 +275,15 @@ int als_factor_stride(const als_engine* e) { return e ? e->kp : 0; }
 
 namespace {
 
+int ensure_stage(als_engine* e) {
+    constexpr size_t STAGE = 32u << 20;
+    if (!e->h_stage) {
+        HIP_TRY(hipHostMalloc(&e->h_stage, STAGE, hipHostMallocDefault));
+        e->stage_bytes = STAGE;
+    }
+    return ALS_OK;
+}
+
 int check_block_shape(als_engine* e, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows) {
     if (n_rows < 0 || row_offset < 0 || n_opp_rows < 0)
         return fail(ALS_ERR_INVALID_ARGUMENT, "negative size (n_rows=%lld row_offset=%lld n_opp_rows=%lld)",
@@ -254,14 +295,23 @@ int check_block_shape(als_engine* e, int64_t n_rows, int64_t row_offset, int64_t
     return ALS_OK;
 }
 
+int max_abs_rating(const int16_t* r, int64_t n) {
+    int m = 0;
+    for (int64_t i = 0; i < n; ++i) m = std::max(m, std::abs((int)r[i]));
+    return m;
+}
+
 // Padded entries of a row of degree d (every row starts on a 32-entry block).
 inline int64_t padded(int64_t d) { return (d + cfk::BLOCK_ENTRIES - 1) / cfk::BLOCK_ENTRIES * cfk::BLOCK_ENTRIES; }
 
 // Work plan of a block whose padded in-block (d_col / d_rat, device, already laid out) has row degrees deg[]
 // and row starts begin[]: FULL / PARTIAL / REDUCE tasks, longest first; uploads the plan, takes ownership of
 // d_col / d_rat and sizes the partial and pre-split workspaces.
+// max_abs_rating: largest |rating| of the block (the pre-split Gram feeds ratings to a bf16 MFMA operand, exact
+// only for |r| <= 256; the reference accepts any Java short, NetflixDataFormatProducer.java:50).
 int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows, int64_t nnz,
-                 const std::vector<int64_t>& deg, const std::vector<int64_t>& begin, int32_t* d_col, float* d_rat) {
+                 const std::vector<int64_t>& deg, const std::vector<int64_t>& begin, int32_t* d_col, float* d_rat,
+                 int max_abs_rating) {
     const int64_t nnz_padded = begin[n_rows];
     auto drop = [&]() {
         (void)hipFree(d_col);
@@ -337,6 +387,9 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
         bool ps = e->path == Path::MFMA_SPLIT && e->kp == 64 && sb <= (8ll << 20);
         if (const char* env = getenv("ALS_PRESPLIT")) ps = e->path == Path::MFMA_SPLIT && e->kp == 64 && env[0] == '1';
         if (n_opp_rows + 1 >= (1 << 24)) ps = false;   // 24-bit row offsets in the pre-split gather
+        // its RHS multiplies bf16 ratings: integers beyond +-256 are not all bf16 (257 -> 256), so such blocks
+        // take the fp32 VALU RHS of the on-the-fly split path instead
+        if (max_abs_rating > 256) ps = false;
         blk.presplit = ps;
         if (ps && (size_t)sb > e->split_bytes) {
             (void)hipFree(e->d_split);
@@ -429,7 +482,8 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
             return fail(ALS_ERR_OUT_OF_MEMORY, "in-block upload: %s", hipGetErrorString(st));
         }
     }
-    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat);
+    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat,
+                        max_abs_rating(ratings, nnz));
 }
 
 int als_set_block_coo(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows, int64_t nnz,
@@ -448,7 +502,8 @@ int als_set_block_coo(als_engine* e, int side, int64_t n_rows, int64_t row_offse
     const int code = cfk::build_block_device(rows, cols, ratings, nnz, n_rows, n_opp_rows, e->stream, deg, begin,
                                              &d_col, &d_rat, err);
     if (code != ALS_OK) return fail(code, "als_set_block_coo: %s", err.c_str());
-    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat);
+    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat,
+                        max_abs_rating(ratings, nnz));
 }
 
 int als_alloc_factors(als_engine* e, int side, int64_t n_total_rows) {
@@ -478,8 +533,11 @@ int als_bind_factors(als_engine* e, int side, void* device_ptr, int64_t n_total_
     f.ptr = device_ptr;
     f.n_rows = n_total_rows;
     f.owned = false;
-    // the sentinel row after the last factor row must read as zeros (padding entries gather it)
+    // the sentinel row after the last factor row must read as zeros (padding entries gather it). The buffer's
+    // owner may still have work on it queued on another stream (e.g. torch's zero fill): drain the device first,
+    // so the memset and every later engine access are ordered after it.
     HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemsetAsync((char*)device_ptr + (size_t)n_total_rows * e->kp * e->elem(), 0, (size_t)e->kp * e->elem(),
                            e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -506,13 +564,10 @@ int als_write_factors(als_engine* e, int side, int64_t row0, int64_t n_rows, con
     HIP_TRY(hipSetDevice(e->device));
     const size_t es = e->elem();
     // Rows are packed kp wide (padding columns zero) into pinned staging and written by a copy kernel
-    // (cfk::launch_upload), never by SDMA: see the note at upload16 in als_kernels.hip.
+    // (cfk::launch_upload) on the engine's stream: see copy16 in als_kernels.hip.
     const size_t row_bytes = (size_t)e->kp * es;
-    constexpr size_t STAGE = 32u << 20;
-    if (!e->h_stage) {
-        HIP_TRY(hipHostMalloc(&e->h_stage, STAGE, hipHostMallocDefault));
-        e->stage_bytes = STAGE;
-    }
+    if (int r = ensure_stage(e)) return r;
+    HIP_TRY(hipStreamSynchronize(e->stream));   // the staging buffer may still feed an earlier copy
     const int64_t rows_per = (int64_t)(e->stage_bytes / row_bytes);
     for (int64_t r = 0; r < n_rows; r += rows_per) {
         const int64_t nr = std::min(rows_per, n_rows - r);
@@ -539,10 +594,23 @@ int als_read_factors(als_engine* e, int side, int64_t row0, int64_t n_rows, void
     if (n_rows == 0) return ALS_OK;
     if (!host_dst) return fail(ALS_ERR_INVALID_ARGUMENT, "host_dst is NULL");
     HIP_TRY(hipSetDevice(e->device));
+    if (int r = sync_checked(e)) return r;
     const size_t es = e->elem();
-    const char* src = (const char*)f.ptr + (size_t)row0 * e->kp * es;
-    HIP_TRY(hipMemcpy2DAsync(host_dst, dst_ld * es, src, e->kp * es, e->k * es, n_rows, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    // Read back the way the kernels wrote: a copy kernel (cfk::launch_download) moves whole kp-wide rows into
+    // pinned staging, the host keeps the first k columns; the same path as als_write_factors in reverse.
+    const size_t row_bytes = (size_t)e->kp * es;
+    if (int r = ensure_stage(e)) return r;
+    const int64_t rows_per = (int64_t)(e->stage_bytes / row_bytes);
+    for (int64_t r = 0; r < n_rows; r += rows_per) {
+        const int64_t nr = std::min(rows_per, n_rows - r);
+        HIP_TRY(cfk::launch_download((const char*)f.ptr + (size_t)(row0 + r) * row_bytes, e->h_stage,
+                                     (size_t)nr * row_bytes, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        const char* stage = (const char*)e->h_stage;
+        char* dst = (char*)host_dst + (size_t)r * dst_ld * es;
+        for (int64_t i = 0; i < nr; ++i)
+            std::memcpy(dst + (size_t)i * dst_ld * es, stage + i * row_bytes, (size_t)e->k * es);
+    }
     return ALS_OK;
 }
 
@@ -576,6 +644,9 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
     a.lambda = lambda;
     a.sentinel = (int32_t)b.n_opp_rows;
     a.flags = e->path == Path::VALU ? 0 : e->debug_flags;
+    if (++e->gen == 0) e->gen = 1;
+    a.gen = e->debug_fixed_gen ? 1u : e->gen;
+    a.integrity = e->d_integrity;
     TimingRec rec{side, {nullptr, nullptr, nullptr}};
     if (e->timing) {
         for (auto& ev : rec.ev) {
@@ -592,12 +663,13 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
         HIP_TRY(cfk::launch_presplit((const float*)opp.ptr, e->d_split, b.n_opp_rows + 1, e->stream));
         a.opp_split = e->d_split;
     }
-    HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves, b.presplit));
+    HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves, b.presplit, false));
     if (e->timing) HIP_TRY(hipEventRecord(rec.ev[1], e->stream));
     if (n_reduce > 0) {
         a.tasks = reduce;
         a.n_tasks = n_reduce;
-        HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves, b.presplit));
+        a.gen += e->debug_gen_skew;
+        HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves, false, true));
     }
     if (e->timing) {
         HIP_TRY(hipEventRecord(rec.ev[2], e->stream));
@@ -708,7 +780,7 @@ int als_predict(als_engine* e, const int64_t* user_rows, int64_t n_users, const 
     if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
     cleanup();
     if (st != hipSuccess) return fail(ALS_ERR_DEVICE, "als_predict: %s", hipGetErrorString(st));
-    return ALS_OK;
+    return sync_checked(e);
 }
 
 int als_sq_error(als_engine* e, int side, double* sum_sq_error, int64_t* count) {
@@ -734,7 +806,7 @@ int als_sq_error(als_engine* e, int side, double* sum_sq_error, int64_t* count) 
     std::vector<double> se(b.n_tasks);
     if (b.n_tasks > 0)
         HIP_TRY(hipMemcpyAsync(se.data(), b.d_task_se, se.size() * sizeof(double), hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (int r = sync_checked(e)) return r;
     double s = 0.0;
     for (double v : se) s += v;   // fixed (task) order: deterministic
     if (sum_sq_error) *sum_sq_error = s;
@@ -745,7 +817,17 @@ int als_sq_error(als_engine* e, int side, double* sum_sq_error, int64_t* count) 
 int als_synchronize(als_engine* e) {
     if (int r = check_engine(e)) return r;
     HIP_TRY(hipSetDevice(e->device));
+    return sync_checked(e);
+}
+
+int als_integrity_status(als_engine* e, uint32_t* record, int reset) {
+    if (int r = check_engine(e)) return r;
+    HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    uint32_t rec[cfk::INTEGRITY_WORDS];
+    HIP_TRY(hipMemcpy(rec, e->d_integrity, sizeof(rec), hipMemcpyDeviceToHost));
+    if (record) std::memcpy(record, rec, sizeof(rec));
+    if (reset) HIP_TRY(hipMemset(e->d_integrity, 0, sizeof(rec)));
     return ALS_OK;
 }
 
@@ -780,6 +862,16 @@ int als_timing_collect(als_engine* e, int side, double* ms_gram, double* ms_redu
     if (ms_gram) *ms_gram = g;
     if (ms_reduce) *ms_reduce = rd;
     if (n_calls) *n_calls = n;
+    return ALS_OK;
+}
+
+int als_debug_copy_partials(als_engine* e, void* host_dst, int64_t max_bytes, int64_t* bytes) {
+    if (int r = check_engine(e)) return r;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    const int64_t n = std::min<int64_t>(max_bytes, (int64_t)e->partial_bytes);
+    if (bytes) *bytes = (int64_t)e->partial_bytes;
+    if (host_dst && n > 0) HIP_TRY(hipMemcpy(host_dst, e->d_partials, (size_t)n, hipMemcpyDeviceToHost));
     return ALS_OK;
 }
 

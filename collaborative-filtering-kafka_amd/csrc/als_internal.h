@@ -56,7 +56,12 @@ struct SolveArgs {
     int32_t sentinel;       // index of the opposite side's all-zero sentinel row (= n_opp_rows)
     int32_t flags;          // SOLVE_FLAG_* (diagnostics only; 0 in production)
     const void* opp_split;  // MFMA_SPLIT + presplit: the opposite table as bf16 h/m/l pieces (als_presplit)
+    uint32_t gen;           // launch generation (PARTIAL and its REDUCE share it): keys the partial-slot encoding
+    uint32_t* integrity;    // device record of partial slots that failed their check (see als_kernels.hip)
 };
+// Partial-slot integrity record (device, 4 words): [0] REDUCE tasks that found a bad slot, [1] generation, [2] slot,
+// [3] row of the first failure. Read back by every synchronising call of the engine.
+constexpr int INTEGRITY_WORDS = 4;
 // Diagnostic: skip the k x k solve after the Gram (stores the Gram diagonal instead) -- used by
 // tools/kbench.py to split a launch's time into Gram and solve. Never set on the product path.
 constexpr int32_t SOLVE_FLAG_SKIP_SOLVE = 1;
@@ -81,8 +86,9 @@ enum class Path : int { VALU = 0, MFMA = 1, MFMA_SPLIT = 2 };
 
 // Launch helpers (defined in als_kernels.hip). Return hipSuccess or the launch error.
 // min_waves: occupancy target (waves per SIMD) of the MFMA variant (__launch_bounds__ second argument).
+// reduce: `a.tasks` are REDUCE tasks (launched after the FULL/PARTIAL launch of the same half).
 hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, int min_waves,
-                        bool presplit = false);
+                        bool presplit, bool reduce);
 // Pre-split of an fp32 [n_rows][64] factor table (sentinel row included) into the bf16 h/m/l piece layout
 // the presplit Gram gathers: row r, lane piece j (features 4j..4j+3) = 6 dwords at byte r*384 + j*24:
 // h(f0,f1) h(f2,f3) m(f0,f1) m(f2,f3) l(f0,f1) l(f2,f3).
@@ -90,6 +96,7 @@ constexpr int PRESPLIT_ROW_BYTES = 384;
 hipError_t launch_presplit(const float* src, void* dst, int64_t n_rows, hipStream_t s);
 // bytes % 16 == 0; host_pinned must stay valid until the stream has passed the copy
 hipError_t launch_upload(const void* host_pinned, void* dst, size_t bytes, hipStream_t s);
+hipError_t launch_download(const void* src, void* host_pinned, size_t bytes, hipStream_t s);
 // out[u][m] = Java-float dot of U row urows[u] and M row mrows[m] (device arrays; out row-major n_u x n_m).
 hipError_t launch_predict(int precision, const void* U, const void* M, int kp, int k, const int64_t* urows,
                           int64_t n_u, const int64_t* mrows, int64_t n_m, float* out, hipStream_t s);

@@ -102,6 +102,80 @@ __device__ __forceinline__ Task load_task(const Task* p) {
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Partial-slot integrity. A PARTIAL task stores word w of lane l of slot s as bits ^ key(gen, s, l, w) plus
+// one check word (the wrap-around sum of the plain words); its REDUCE task decodes with the SAME launch
+// generation and re-sums. A slot line the REDUCE cannot see freshly written -- never written, left over
+// from an earlier launch (which, on identical inputs, would hold identical numbers and be invisible to any
+// comparison of results), or torn -- decodes to noise and fails the check; the failure is counted in
+// SolveArgs::integrity and the engine's next synchronising call reports it (ALS_ERR_INTEGRITY).
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ uint32_t slot_key(uint32_t gen, int32_t slot, int lane) {
+    return mix32(gen * 0x9e3779b1u ^ mix32((uint32_t)slot * 64u + (uint32_t)lane));
+}
+constexpr uint32_t WORD_KEY_STEP = 0x632be5abu;
+struct SlotCodec {
+    uint32_t key, sum = 0;
+    __device__ __forceinline__ float enc(float v, int w) {
+        const uint32_t b = __float_as_uint(v);
+        sum += b;
+        return __uint_as_float(b ^ (key + (uint32_t)w * WORD_KEY_STEP));
+    }
+    __device__ __forceinline__ float dec(float v, int w) {
+        const uint32_t b = __float_as_uint(v) ^ (key + (uint32_t)w * WORD_KEY_STEP);
+        sum += b;
+        return __uint_as_float(b);
+    }
+    __device__ __forceinline__ double enc(double v, int w) {
+        const uint64_t b = (uint64_t)__double_as_longlong(v);
+        sum += (uint32_t)b + (uint32_t)(b >> 32);
+        const uint64_t k = key + (uint32_t)w * WORD_KEY_STEP;
+        return __longlong_as_double((long long)(b ^ (k | (k << 32))));
+    }
+    __device__ __forceinline__ double dec(double v, int w) {
+        const uint64_t k = key + (uint32_t)w * WORD_KEY_STEP;
+        const uint64_t b = (uint64_t)__double_as_longlong(v) ^ (k | (k << 32));
+        sum += (uint32_t)b + (uint32_t)(b >> 32);
+        return __longlong_as_double((long long)b);
+    }
+    // check word (element w of the slot), stored keyed like the data words
+    template <class T>
+    __device__ __forceinline__ T check_word(int w) const {
+        const uint32_t c = sum ^ (key + (uint32_t)w * WORD_KEY_STEP);
+        if constexpr (sizeof(T) == 4) return __uint_as_float(c);
+        else return __longlong_as_double((long long)(uint64_t)c);
+    }
+    template <class T>
+    __device__ __forceinline__ bool check_ok(T stored, int w) const {
+        uint32_t c;
+        if constexpr (sizeof(T) == 4) c = __float_as_uint(stored);
+        else c = (uint32_t)(uint64_t)__double_as_longlong(stored);
+        return (c ^ (key + (uint32_t)w * WORD_KEY_STEP)) == sum;
+    }
+};
+// Vector-memory atomics only, from the first failing lane (slot = the first slot that lane found bad).
+__device__ __forceinline__ void report_bad_slot(uint32_t* rec, uint32_t gen, int32_t slot, int32_t row, bool bad,
+                                                int lane) {
+    const uint64_t m = __ballot(bad);
+    if (m == 0) return;
+    if (lane == (int)__builtin_ctzll(m)) {
+        const uint32_t n = atomicAdd(rec, 1u);
+        if (n == 0) {
+            atomicExch(rec + 1, gen);
+            atomicExch(rec + 2, (uint32_t)slot);
+            atomicExch(rec + 3, (uint32_t)row);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
 // Per-wave LDS carve-up
 // ---------------------------------------------------------------------------------------------------
 __host__ __device__ constexpr int round16(int b) { return (b + 15) & ~15; }
@@ -707,7 +781,9 @@ __global__ __launch_bounds__(256) void als_presplit(const float* __restrict__ sr
     *(u32x2*)(o + 4) = u32x2{l01, l23};
 }
 
-template <int KP, int MINW, bool SPLIT, bool PRESPLIT = false>
+// REDUCE = true: the launch of a half's REDUCE tasks (sum of partial slots + solve), compiled apart from the
+// gather kernel so neither carries the other's code and registers.
+template <int KP, int MINW, bool SPLIT, bool PRESPLIT = false, bool REDUCE = false>
 __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(SolveArgs a) {
     constexpr int C = KP / 16;
     constexpr int NW = mfma_waves<KP>();
@@ -734,17 +810,25 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
     for (int c = 0; c < C; ++c) E[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     float* part = (float*)a.partials;
-    if (tk.kind == TASK_REDUCE) {
-        // Fixed-order sum of the row's partial slots ([word][lane] layout, coalesced).
+    constexpr int SLOT_WORDS = Acc::NWORDS + 1;   // + integrity check word
+    if constexpr (REDUCE) {
+        // Fixed-order sum of the row's partial slots ([word][lane] layout, coalesced), each decoded and checked.
+        bool bad = false;
+        int32_t bad_slot = -1;
         for (int s = 0; s < tk.nsteps; ++s) {
-            const float* src = part + (int64_t)(tk.slot + s) * (Acc::NWORDS * 64) + lane;
+            const float* src = part + (int64_t)(tk.slot + s) * (SLOT_WORDS * 64) + lane;
+            SlotCodec cd{slot_key(a.gen, tk.slot + s, lane)};
 #pragma unroll
             for (int p = 0; p < Acc::NT; ++p)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc.g[p][r] += src[(p * 4 + r) * 64];
+                for (int r = 0; r < 4; ++r) acc.g[p][r] += cd.dec(src[(p * 4 + r) * 64], p * 4 + r);
 #pragma unroll
-            for (int c = 0; c < C; ++c) acc.rhs[c] += src[(Acc::NT * 4 + c) * 64];
+            for (int c = 0; c < C; ++c) acc.rhs[c] += cd.dec(src[(Acc::NT * 4 + c) * 64], Acc::NT * 4 + c);
+            const bool ok = cd.check_ok(src[Acc::NWORDS * 64], Acc::NWORDS);
+            if (!ok && !bad) bad_slot = tk.slot + s;
+            bad |= !ok;
         }
+        report_bad_slot(a.integrity, a.gen, bad_slot, tk.row, bad, lane);
     } else {
         // Gather pipeline over blocks of B = 8 sub-steps (32 entries, layout [g][t], see block_position):
         // lane (g, j) loads the 8 column indices / ratings of its group with two 16-B loads, issued one
@@ -789,8 +873,8 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             // Split-bf16 Gram over a PRE-SPLIT opposite table (als_presplit, once per half): lane (g, j) loads
             // the 24-B h/m/l piece of features 4j..4j+3 of its group's 8 entries and only transposes bf16
             // halves into the MFMA operands (v_perm_b32: 48 per block instead of ~150 split instructions).
-            // The RHS Y^T r becomes 12 more MFMAs (ratings 1..5 are exact in bf16; B[k][*] = r_k, so every
-            // column of the result holds Y_b^T r). Chosen for tables that stay L2-resident (the 17,770-row
+            // The RHS Y^T r becomes 12 more MFMAs (B[k][*] = r_k, so every column of the result holds Y_b^T r;
+            // the engine picks this variant only for blocks whose ratings are exact in bf16, |r| <= 256). Chosen for tables that stay L2-resident (the 17,770-row
             // movie table the user half reads): 1.5x the gathered bytes, far fewer VALU instructions.
             static_assert(C == 4, "pre-split Gram: KP = 64");
             typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -1126,17 +1210,19 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
     }
 
     if constexpr (SPLIT && CFK_DIAG_SYM) {
-        if (tk.kind != TASK_REDUCE) fold_diag<C>(acc, E, lane);
+        if constexpr (!REDUCE) fold_diag<C>(acc, E, lane);
     }
 
-    if (tk.kind == TASK_PARTIAL) {
-        float* dst = part + (int64_t)tk.slot * (Acc::NWORDS * 64) + lane;
+    if (!REDUCE && tk.kind == TASK_PARTIAL) {
+        float* dst = part + (int64_t)tk.slot * (SLOT_WORDS * 64) + lane;
+        SlotCodec cd{slot_key(a.gen, tk.slot, lane)};
 #pragma unroll
         for (int p = 0; p < Acc::NT; ++p)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dst[(p * 4 + r) * 64] = acc.g[p][r];
+            for (int r = 0; r < 4; ++r) dst[(p * 4 + r) * 64] = cd.enc(acc.g[p][r], p * 4 + r);
 #pragma unroll
-        for (int c = 0; c < C; ++c) dst[(Acc::NT * 4 + c) * 64] = acc.rhs[c];
+        for (int c = 0; c < C; ++c) dst[(Acc::NT * 4 + c) * 64] = cd.enc(acc.rhs[c], Acc::NT * 4 + c);
+        dst[Acc::NWORDS * 64] = cd.check_word<float>(Acc::NWORDS);
         return;
     }
 
@@ -1194,13 +1280,21 @@ __global__ __launch_bounds__(256) void als_solve_valu(SolveArgs a) {
     T rhs = T(0);
 
     T* part = (T*)a.partials;
+    constexpr int SLOT_WORDS = NWORDS + 1;   // + integrity check word (SlotCodec)
     if (tk.kind == TASK_REDUCE) {
+        bool bad = false;
+        int32_t bad_slot = -1;
         for (int s = 0; s < tk.nsteps; ++s) {
-            const T* src = part + (int64_t)(tk.slot + s) * (NWORDS * 64) + lane;
+            const T* src = part + (int64_t)(tk.slot + s) * (SLOT_WORDS * 64) + lane;
+            SlotCodec cd{slot_key(a.gen, tk.slot + s, lane)};
 #pragma unroll
-            for (int e = 0; e < E; ++e) acc[e] += src[e * 64];
-            rhs += src[E * 64];
+            for (int e = 0; e < E; ++e) acc[e] += cd.dec(src[e * 64], e);
+            rhs += cd.dec(src[E * 64], E);
+            const bool ok = cd.check_ok(src[NWORDS * 64], NWORDS);
+            if (!ok && !bad) bad_slot = tk.slot + s;
+            bad |= !ok;
         }
+        report_bad_slot(a.integrity, a.gen, bad_slot, tk.row, bad, lane);
     } else {
         const T* opp = (const T*)a.opp;
         const int n = (tk.nsteps + BLOCK_SUBSTEPS - 1) / BLOCK_SUBSTEPS * BLOCK_ENTRIES;   // task span
@@ -1235,10 +1329,12 @@ __global__ __launch_bounds__(256) void als_solve_valu(SolveArgs a) {
     }
 
     if (tk.kind == TASK_PARTIAL) {
-        T* dst = part + (int64_t)tk.slot * (NWORDS * 64) + lane;
+        T* dst = part + (int64_t)tk.slot * (SLOT_WORDS * 64) + lane;
+        SlotCodec cd{slot_key(a.gen, tk.slot, lane)};
 #pragma unroll
-        for (int e = 0; e < E; ++e) dst[e * 64] = acc[e];
-        dst[E * 64] = rhs;
+        for (int e = 0; e < E; ++e) dst[e * 64] = cd.enc(acc[e], e);
+        dst[E * 64] = cd.enc(rhs, E);
+        dst[NWORDS * 64] = cd.check_word<T>(NWORDS);
         return;
     }
 
@@ -1329,13 +1425,17 @@ __global__ __launch_bounds__(256) void als_predict_kernel(const T* __restrict__ 
 int blocks_for(int n_tasks) { return (n_tasks + WAVES - 1) / WAVES; }
 
 template <class T, int KP, Path P, int MINW = 1, bool PRESPLIT = false>
-hipError_t launch_solve_t(const SolveArgs& a, hipStream_t s) {
+hipError_t launch_solve_t(const SolveArgs& a, hipStream_t s, bool reduce) {
     if (a.n_tasks <= 0) return hipSuccess;
     constexpr int bytes = WAVES * WaveLds<T, KP, P>::BYTES;
     if constexpr (P == Path::MFMA || P == Path::MFMA_SPLIT) {
         static_assert(std::is_same<T, float>::value, "MFMA paths are fp32");
         constexpr int nw = mfma_waves<KP>();
-        als_solve_mfma<KP, MINW, P == Path::MFMA_SPLIT, PRESPLIT><<<(a.n_tasks + nw - 1) / nw, 64 * nw, 0, s>>>(a);
+        const unsigned grid = (unsigned)((a.n_tasks + nw - 1) / nw);
+        if (reduce)   // one REDUCE kernel per KP: the partial slots have the same layout on every Gram path
+            als_solve_mfma<KP, MINW, false, false, true><<<grid, 64 * nw, 0, s>>>(a);
+        else
+            als_solve_mfma<KP, MINW, P == Path::MFMA_SPLIT, PRESPLIT><<<grid, 64 * nw, 0, s>>>(a);
     } else {
         static bool attr = false;
         if (!attr) {
@@ -1369,9 +1469,9 @@ bool variant_available(int precision, int kp, Path path) {
 int partial_words_per_lane(int precision, int kp, Path path) {
     if (path == Path::MFMA || path == Path::MFMA_SPLIT) {
         const int c = kp / 16;
-        return (c * (c + 1) / 2) * 4 + c;
+        return (c * (c + 1) / 2) * 4 + c + 1;   // accumulators + RHS + check word
     }
-    return kp * kp / 64 + 1;
+    return kp * kp / 64 + 1 + 1;
 }
 
 hipError_t launch_predict(int precision, const void* U, const void* M, int kp, int k, const int64_t* urows,
@@ -1387,23 +1487,32 @@ hipError_t launch_predict(int precision, const void* U, const void* M, int kp, i
     return hipGetLastError();
 }
 
-// Host -> device upload as a KERNEL write: each lane reads 16 B of pinned host memory (zero-copy, non-temporal)
-// and stores it to device memory through L2 -- the same coherence path as the solve kernels' own writes. Used
-// for factor tables: an SDMA copy over memory that kernels wrote (and may still hold in an XCD's L2) was
-// observed to leave stale rows for the next solve (tests/test_gpu_parity.py::test_bitwise_determinism...).
-__global__ __launch_bounds__(256) void upload16(const u32x4* __restrict__ src, u32x4* __restrict__ dst, int64_t n) {
+// Host <-> device factor-table copies as KERNEL accesses: each lane moves 16 B between pinned host memory
+// (zero-copy, non-temporal) and device memory, so the factor tables are only ever written and read through
+// the same cache path as the solve kernels' own accesses (no SDMA engine in between). This keeps every access
+// to a factor table on one documented ordering path: kernels on the engine's stream.
+__global__ __launch_bounds__(256) void copy16(const u32x4* __restrict__ src, u32x4* __restrict__ dst, int64_t n,
+                                              int to_host) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        dst[i] = __builtin_nontemporal_load(src + i);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (to_host) __builtin_nontemporal_store(src[i], dst + i);
+        else dst[i] = __builtin_nontemporal_load(src + i);
+    }
 }
 
-hipError_t launch_upload(const void* host_pinned, void* dst, size_t bytes, hipStream_t s) {
+hipError_t launch_copy(const void* src, void* dst, size_t bytes, int to_host, hipStream_t s) {
     if (bytes == 0) return hipSuccess;
     if (bytes % 16 != 0) return hipErrorInvalidValue;
     const int64_t n = (int64_t)(bytes / 16);
     const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
-    upload16<<<(unsigned)blocks, 256, 0, s>>>((const u32x4*)host_pinned, (u32x4*)dst, n);
+    copy16<<<(unsigned)blocks, 256, 0, s>>>((const u32x4*)src, (u32x4*)dst, n, to_host);
     return hipGetLastError();
+}
+hipError_t launch_upload(const void* host_pinned, void* dst, size_t bytes, hipStream_t s) {
+    return launch_copy(host_pinned, dst, bytes, 0, s);
+}
+hipError_t launch_download(const void* src, void* host_pinned, size_t bytes, hipStream_t s) {
+    return launch_copy(src, host_pinned, bytes, 1, s);
 }
 
 hipError_t launch_presplit(const float* src, void* dst, int64_t n_rows, hipStream_t s) {
@@ -1414,27 +1523,27 @@ hipError_t launch_presplit(const float* src, void* dst, int64_t n_rows, hipStrea
 }
 
 hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, int min_waves,
-                        bool presplit) {
+                        bool presplit, bool reduce) {
     if (precision == 0) {
         if (path == Path::MFMA) {
-            if (kp == 32) return launch_solve_t<float, 32, Path::MFMA, 2>(a, s);
-            if (kp == 64 && min_waves >= 3) return launch_solve_t<float, 64, Path::MFMA, 3>(a, s);
-            if (kp == 64) return launch_solve_t<float, 64, Path::MFMA, 2>(a, s);
-            if (kp == 128) return launch_solve_t<float, 128, Path::MFMA, 1>(a, s);
+            if (kp == 32) return launch_solve_t<float, 32, Path::MFMA, 2>(a, s, reduce);
+            if (kp == 64 && min_waves >= 3) return launch_solve_t<float, 64, Path::MFMA, 3>(a, s, reduce);
+            if (kp == 64) return launch_solve_t<float, 64, Path::MFMA, 2>(a, s, reduce);
+            if (kp == 128) return launch_solve_t<float, 128, Path::MFMA, 1>(a, s, reduce);
         } else if (path == Path::MFMA_SPLIT) {
-            if (kp == 32) return launch_solve_t<float, 32, Path::MFMA_SPLIT, 2>(a, s);
-            if (kp == 64 && presplit) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2, true>(a, s);
-            if (kp == 64) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2>(a, s);
-            if (kp == 128) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1>(a, s);
+            if (kp == 32) return launch_solve_t<float, 32, Path::MFMA_SPLIT, 2>(a, s, reduce);
+            if (kp == 64 && presplit) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2, true>(a, s, reduce);
+            if (kp == 64) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2>(a, s, reduce);
+            if (kp == 128) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1>(a, s, reduce);
         } else {
-            if (kp == 16) return launch_solve_t<float, 16, Path::VALU>(a, s);
-            if (kp == 32) return launch_solve_t<float, 32, Path::VALU>(a, s);
-            if (kp == 64) return launch_solve_t<float, 64, Path::VALU>(a, s);
+            if (kp == 16) return launch_solve_t<float, 16, Path::VALU>(a, s, reduce);
+            if (kp == 32) return launch_solve_t<float, 32, Path::VALU>(a, s, reduce);
+            if (kp == 64) return launch_solve_t<float, 64, Path::VALU>(a, s, reduce);
         }
     } else if (path == Path::VALU) {
-        if (kp == 16) return launch_solve_t<double, 16, Path::VALU>(a, s);
-        if (kp == 32) return launch_solve_t<double, 32, Path::VALU>(a, s);
-        if (kp == 64) return launch_solve_t<double, 64, Path::VALU>(a, s);
+        if (kp == 16) return launch_solve_t<double, 16, Path::VALU>(a, s, reduce);
+        if (kp == 32) return launch_solve_t<double, 32, Path::VALU>(a, s, reduce);
+        if (kp == 64) return launch_solve_t<double, 64, Path::VALU>(a, s, reduce);
     }
     return hipErrorInvalidValue;
 }

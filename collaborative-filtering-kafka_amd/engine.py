@@ -256,6 +256,10 @@ class ALSEngine:
         self._h = h
         self.kp = _lib.lib().als_factor_stride(self._h)
         self.factors = [None, None]    # torch tensors [n_slots, kp]
+        # the factor tables are torch tensors (torch.zeros fill, RCCL all-gathers): launch on torch's current
+        # stream from the start so every access is ordered (als.h ordering contract); set_stream-style calls
+        # may move it later
+        self.use_torch_stream()
 
     def close(self):
         if self._h and self._h.value:
@@ -351,6 +355,12 @@ class ALSEngine:
     def synchronize(self):
         call("als_synchronize", self._h)
 
+    def integrity_status(self, reset: bool = False) -> list[int]:
+        """[REDUCE tasks that found a bad slot, generation, slot, row] of the first failure (0s when none)."""
+        rec = (ctypes.c_uint32 * 4)()
+        call("als_integrity_status", self._h, rec, 1 if reset else 0)
+        return list(rec)
+
     def set_timing(self, on: bool):
         call("als_set_timing", self._h, 1 if on else 0)
 
@@ -358,6 +368,14 @@ class ALSEngine:
         g, r, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
         call("als_timing_collect", self._h, _side(side), ctypes.byref(g), ctypes.byref(r), ctypes.byref(n))
         return g.value, r.value, n.value
+
+    def debug_partials(self) -> np.ndarray:
+        """The partial-slot workspace as raw 32-bit words (diagnostics)."""
+        n = ctypes.c_int64()
+        call("als_debug_copy_partials", self._h, None, 0, ctypes.byref(n))
+        out = np.zeros(n.value // 4, np.uint32)
+        call("als_debug_copy_partials", self._h, out.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(n))
+        return out
 
     def block_stats(self, side):
         a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()

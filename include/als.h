@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define ALS_ABI_VERSION 1
+#define ALS_ABI_VERSION 2
 
 typedef enum {
     ALS_OK = 0,
@@ -42,7 +42,9 @@ typedef enum {
     ALS_ERR_STATE = 5,         /* call order violated (e.g. solve before a block was set) */
     ALS_ERR_IO = 6,
     ALS_ERR_PARSE = 7,
-    ALS_ERR_DATA = 8           /* input that hangs the reference (duplicate pair, count mismatch) */
+    ALS_ERR_DATA = 8,          /* input that hangs the reference (duplicate pair, count mismatch) */
+    ALS_ERR_INTEGRITY = 9      /* a split row's REDUCE task read a partial slot this launch had not written
+                                  (als_integrity_status); the results of that half are not trustworthy */
 } als_status;
 
 typedef enum { ALS_SIDE_MOVIE = 0, ALS_SIDE_USER = 1 } als_side;
@@ -59,7 +61,10 @@ const char* als_last_error(void);
  * num_features = ALSApp.NUM_FEATURES (ALSApp.java:18), 1..128 (f64: 1..64). */
 int als_engine_create(int device, int num_features, int precision, als_engine** out);
 int als_engine_destroy(als_engine* e);
-/* Launch on a caller-provided hipStream_t (e.g. torch's current stream); NULL = engine-owned stream. */
+/* Launch on a caller-provided hipStream_t (e.g. torch's current stream); NULL = engine-owned stream.
+ * Ordering contract: the engine orders its own work on its stream only. A caller that reads or writes a bound
+ * factor buffer (als_bind_factors) from other work -- torch ops, RCCL collectives -- must issue that work on
+ * the engine's stream or synchronise (als_synchronize) in between. */
 int als_engine_set_stream(als_engine* e, void* hip_stream);
 /* Launch on the device's NULL (legacy default) stream: the stream torch launches on when no other stream is
  * current (its handle is 0, which als_engine_set_stream would read as "engine-owned"). The engine's kernels are
@@ -125,12 +130,21 @@ int als_predict(als_engine* e, const int64_t* user_rows, int64_t n_users, const 
  * reduction of scripts/calculate_mse.py:78-90 computed on the device from the factors). Synchronous. */
 int als_sq_error(als_engine* e, int side, double* sum_sq_error, int64_t* count);
 
+/* Waits for the engine's stream. Like every synchronising call (als_read_factors, als_sq_error, als_predict)
+ * it returns ALS_ERR_INTEGRITY once a REDUCE task has found a partial slot that its PARTIAL task's writes had
+ * not reached (each slot is stored keyed by the launch generation with a check word). */
 int als_synchronize(als_engine* e);
+/* The integrity record: record[0] = REDUCE tasks that found a bad slot so far, record[1..3] = launch generation, slot
+ * and local row of the first; reset != 0 clears it. Synchronising. */
+int als_integrity_status(als_engine* e, uint32_t* record, int reset);
 /* Device-time accounting with HIP events on the engine's stream (non-blocking while enabled): every
  * als_solve_half records its gram/solve launch and its reduce launch; als_timing_collect waits for the
  * recorded events of `side`, returns their summed milliseconds and call count, and clears them. */
 int als_set_timing(als_engine* e, int enabled);
 int als_timing_collect(als_engine* e, int side, double* ms_gram, double* ms_reduce, int64_t* n_calls);
+/* Diagnostics: copies up to max_bytes of the partial-slot workspace (the PARTIAL tasks' encoded sums of the
+ * last half) to host memory and reports its size. Synchronising. */
+int als_debug_copy_partials(als_engine* e, void* host_dst, int64_t max_bytes, int64_t* bytes);
 /* Work-plan statistics of the uploaded block (tasks, partial slots, padded nnz). */
 int als_block_stats(const als_engine* e, int side, int64_t* n_tasks, int64_t* n_reduce, int64_t* nnz_padded);
 

@@ -205,14 +205,24 @@ int oracle_update_rows_f64(int64_t n_sel, const int64_t* sel_rows, const int64_t
                            const int32_t* col_idx, const int16_t* ratings, const double* opp, int k,
                            float lambda, double* out /* n_sel x k */) {
     size_t ws_bytes = sizeof(double) * (2 * (size_t)k * k + 2 * (size_t)k) + sizeof(int) * (size_t)k + 64;
-    double* ws = (double*)malloc(ws_bytes);
-    if (!ws) return 2;
-    for (int64_t s = 0; s < n_sel; ++s) {
-        int64_t r = sel_rows[s];
-        update_row_f64(row_ptr[r], row_ptr[r + 1], col_idx, ratings, opp, k, (double)lambda, out + s * k, ws);
+    int rc = 0;
+#pragma omp parallel
+    {
+        double* ws = (double*)malloc(ws_bytes);
+        if (!ws) {
+#pragma omp atomic write
+            rc = 2;
+        }
+#pragma omp for schedule(dynamic, 1)
+        for (int64_t s = 0; s < n_sel; ++s) {
+            int64_t r = sel_rows[s];
+            if (ws)
+                update_row_f64(row_ptr[r], row_ptr[r + 1], col_idx, ratings, opp, k, (double)lambda, out + s * k,
+                               ws);
+        }
+        free(ws);
     }
-    free(ws);
-    return 0;
+    return rc;
 }
 
 /* ------------------------------------------------------------------------------------------------ */

@@ -1,0 +1,162 @@
+"""GPU parity at the BASELINE.json configurations themselves (not only at test size).
+
+- configs[2]: the full Netflix-shape workload (480,189 x 17,770 x 1e8, k = 64, fp32, 1 GPU). One movie half
+  and one user half through the product path (ALSApp over libcfk_als.so), then sampled rows -- the 20 longest
+  movie rows (split into PARTIAL chunks + a REDUCE task at chunk = nnz/4096), degree-1 users, the longest
+  users and random rows -- against the fp64 oracle (oracle.update_rows_f64, the restatement of
+  MFeatureCalculator.java:66-104 / UFeatureCalculator.java:66-104) and the oracle's fp32 EJML-order restatement
+  (the reference's own fp32 error envelope).
+- configs[4] scaled down: one shard (G = 8) of a power-law matrix whose heaviest items carry >= 100k ratings,
+  with full factor replicas, on one GPU.
+- configs[3]: k = 128 sharded over two ranks with the chunked (overlapped) user half, against the oracle's MSE.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+LAM = 0.05
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _sub_side(oracle_mod, blk, rows):
+    """oracle.Side of the selected CSR rows (their entries in in-block order)."""
+    rp = blk["row_ptr"]
+    deg = np.diff(rp)[rows]
+    sub_rp = np.zeros(len(rows) + 1, np.int64)
+    np.cumsum(deg, out=sub_rp[1:])
+    col = np.concatenate([blk["col"][rp[r]:rp[r + 1]] for r in rows])
+    rat = np.concatenate([blk["ratings"][rp[r]:rp[r + 1]] for r in rows])
+    return oracle_mod.Side(ids=np.asarray(rows, np.int64), row_ptr=sub_rp, col=col, ratings=rat)
+
+
+def _check_rows(oracle_mod, blk, rows, got, opp, what):
+    """fp64 oracle norm-relative error <= 1e-4, and within 3x the reference's own fp32 error on the same rows
+    (test_gpu_parity.test_one_half_every_k_vs_oracle's bar)."""
+    side = _sub_side(oracle_mod, blk, rows)
+    ref = oracle_mod.update_rows_f64(blk["row_ptr"], blk["col"], blk["ratings"], rows, opp.astype(np.float64), LAM)
+    ref32 = oracle_mod.update_side(side, opp.astype(np.float32), LAM, "f32")
+    norm = np.linalg.norm(ref, axis=1)
+    rel = np.linalg.norm(got[rows].astype(np.float64) - ref, axis=1) / norm
+    rel_ref = np.linalg.norm(ref32 - ref, axis=1) / norm
+    bad = rel > np.maximum(1e-4, 3 * rel_ref)
+    assert not bad.any(), (what, [(int(rows[i]), int(np.diff(blk["row_ptr"])[rows[i]]), float(rel[i]),
+                                   float(rel_ref[i])) for i in np.nonzero(bad)[0][:8]])
+    return float(rel.max())
+
+
+def _sample(blk, rng, n_long=20, n_rand=160, extra=()):
+    deg = np.diff(blk["row_ptr"])
+    longest = np.argsort(-deg, kind="stable")[:n_long]
+    rand = rng.choice(len(deg), size=min(n_rand, len(deg)), replace=False)
+    return np.unique(np.concatenate([longest, rand, np.asarray(extra, np.int64)])).astype(np.int64)
+
+
+def test_netflix_shape_full_size_sampled_rows(cfk, oracle_mod):
+    """BASELINE configs[2] at full size through ALSApp (GPU block build, split rows, pre-split user half)."""
+    ds = cfk.Dataset.synthetic_netflix(480_189, 17_770, 100_000_000, 0xA15, nthreads=16)
+    app = cfk.ALSApp(1, 64, LAM, 1, precision="f32", seed=42).setup(ds, check_duplicates=False)
+    eng = app.engine
+    assert eng.block_stats(0)["n_reduce"] > 0                 # the real work plan has split rows
+    U0 = ds.init_user_factors(64, 42)
+    app.movie_half()
+    M = eng.read_factors(0)
+    app.user_half()
+    U = eng.read_factors(1)
+    assert eng.integrity_status() == [0, 0, 0, 0]
+    rng = np.random.default_rng(2024)
+    mblk = ds.shard_block(0)
+    worst_m = _check_rows(oracle_mod, mblk, _sample(mblk, rng), M, U0, "movie")
+    ublk = ds.shard_block(1)
+    udeg = np.diff(ublk["row_ptr"])
+    ones = np.nonzero(udeg == 1)[0][:40]
+    worst_u = _check_rows(oracle_mod, ublk, _sample(ublk, rng, extra=ones), U, M, "user")
+    print(f"configs[2] full size: worst norm-rel movie {worst_m:.2e}, user {worst_u:.2e}")
+
+
+def test_powerlaw_shard_sampled_rows(cfk, oracle_mod):
+    """BASELINE configs[4] scaled down (1M users x 50k items x 5e7 ratings, Zipf items, log-normal sigma 1.5
+    users): shard 0 of G = 8 with full factor replicas, heavy items (>= 100k ratings) split into PARTIAL
+    chunks + REDUCE tasks; sampled rows of both halves against the oracle."""
+    G = 8
+    ds = cfk.Dataset.synthetic_powerlaw(1_000_000, 50_000, 50_000_000, 0xA15, nthreads=16)
+    eng = cfk.ALSEngine(64, "f32")
+    info = [ds.shard_info(s, G, 0) for s in (0, 1)]
+    for side in (0, 1):
+        c = ds.shard_coo(side, G, 0)
+        eng.alloc_factors(side, info[side]["n_slots"])
+        eng.set_block_coo(side, c["n_rows"], c["rows"], c["cols"], c["ratings"], c["row_offset"],
+                          info[1 - side]["n_slots"])
+    mblk = ds.shard_block(0, G, 0)
+    mdeg = np.diff(mblk["row_ptr"])
+    assert mdeg.max() >= 100_000 and eng.block_stats(0)["n_reduce"] > 0
+    rng = np.random.default_rng(7)
+    U0 = ds.init_user_factors(64, 42, G)                       # slot order of G shards
+    eng.write_factors(1, U0)
+    eng.solve_half(0, LAM)
+    Mfull = eng.read_factors(0)
+    M = Mfull[info[0]["row_offset"]:info[0]["row_offset"] + info[0]["n_rows"]]
+    heavy = np.nonzero(mdeg >= 100_000)[0]
+    worst_m = _check_rows(oracle_mod, mblk, _sample(mblk, rng, extra=heavy), M, U0, "item")
+    # user half of the shard against a full random item replica
+    Mr = rng.random((info[0]["n_slots"], 64), dtype=np.float32)
+    eng.write_factors(0, Mr)
+    eng.solve_half(1, LAM)
+    Ufull = eng.read_factors(1)
+    U = Ufull[info[1]["row_offset"]:info[1]["row_offset"] + info[1]["n_rows"]]
+    ublk = ds.shard_block(1, G, 0)
+    worst_u = _check_rows(oracle_mod, ublk, _sample(ublk, rng), U, Mr, "user")
+    assert eng.integrity_status() == [0, 0, 0, 0]
+    eng.close()
+    print(f"configs[4] shard: heaviest item {mdeg.max()} ratings; worst norm-rel item {worst_m:.2e}, "
+          f"user {worst_u:.2e}")
+
+
+def _k128_worker(rank, world, port, out_dir):
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    import __graft_entry__
+    cfk = __graft_entry__.load_package()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ds = cfk.Dataset.synthetic_netflix(n_users=3000, n_movies=400, nnz=90_000, seed=11, nthreads=8)
+    app = cfk.ALSApp(world, 128, LAM, 3, precision="f32", seed=9, device=0, rank=rank, world_size=world,
+                     overlap_chunks=3)
+    app.setup(ds)
+    app.run()
+    U, M = app.factors()
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), U=U, M=M, mse=app.mse())
+    dist.destroy_process_group()
+
+
+def test_sharded_k128_two_ranks_chunked(tmp_path, oracle_mod, cfk):
+    """BASELINE configs[3] path at test size: k = 128 (KP = 128 MFMA variants) sharded over 2 ranks (both on
+    cuda:0, gloo carrying the all-gathers) with the user half in 3 overlapped chunks; MSE delta <= 1e-3 and
+    factors within 1e-3 norm-relative of the fp64 oracle."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_k128_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    ds = cfk.Dataset.synthetic_netflix(n_users=3000, n_movies=400, nnz=90_000, seed=11, nthreads=8)
+    m, u, r = ds.ratings()
+    b = oracle_mod.build_blocks(m, u, r)
+    Uo, Mo = oracle_mod.run_als(b, 128, LAM, 3, seed=9, precision="f64")
+    mse_o = oracle_mod.mse(b, Uo, Mo)
+    for rank in range(2):
+        res = np.load(os.path.join(tmp_path, f"rank{rank}.npz"))
+        assert abs(float(res["mse"]) - mse_o) <= 1e-3
+        assert np.linalg.norm(res["U"] - Uo) / np.linalg.norm(Uo) < 1e-3
+        assert np.linalg.norm(res["M"] - Mo) / np.linalg.norm(Mo) < 1e-3

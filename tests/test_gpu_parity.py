@@ -344,47 +344,77 @@ def test_device_block_build_edge_cases(cfk):
     eng.close()
 
 
-def test_bitwise_determinism_netflix_shape(cfk):
+def _split_slots(deg, nnz_padded):
+    """Partial slots of each split row, as the engine's work plan assigns them (als_engine.cpp chunk_entries /
+    finish_block: rows in order, ceil(deg / chunk) consecutive slots per row longer than chunk)."""
+    c = min(max(nnz_padded // 4096, 1024), 32768)
+    c = (c + 31) // 32 * 32
+    slots, nxt = {}, 0
+    for i, d in enumerate(deg):
+        if d > c:
+            n = -(-int(d) // c)
+            slots[i] = (nxt, nxt + n)
+            nxt += n
+    return slots
+
+
+def test_bitwise_determinism_netflix_shape(cfk, monkeypatch):
     """Full Netflix-shape workload (1e8 ratings, k = 64, split-bf16 Gram, split rows, pre-split movie table):
     each half repeated from identical inputs -- with the other half run in between, which reuses the shared
     partial-slot and pre-split workspaces -- gives bitwise identical factors. (This is the test that caught
-    an MFMA operand hazard at ~20 rows in 17,770; see MFMA_DRAIN in als_kernels.hip.)"""
+    an MFMA operand hazard at ~20 rows in 17,770; see MFMA_DRAIN in als_kernels.hip.) With a fixed launch
+    generation the partial slots of every repetition are bitwise comparable too, so a failure says whether a
+    split row went wrong in its PARTIAL tasks (slots differ) or in its REDUCE task (slots equal)."""
+    monkeypatch.setenv("ALS_DEBUG_FIXED_GEN", "1")
     ds = cfk.Dataset.synthetic_netflix(480_189, 17_770, 100_000_000, 0xA15, nthreads=16)
     U0 = ds.init_user_factors(64, 42)
     eng = cfk.ALSEngine(64, "f32")
-    eng.use_torch_stream()
     for side in (0, 1):
         b = ds.shard_coo(side)
         eng.alloc_factors(side, b["n_slots"])
         eng.set_block_coo(side, b["n_rows"], b["rows"], b["cols"], b["ratings"], 0, ds.shard_info(1 - side)["n_slots"])
-    Ms, Us = [], []
-    for rep in range(3):
+    reps = 6
+    Ms, Us, Ps = [], [], []
+    for rep in range(reps):
         eng.write_factors(1, U0)
         eng.solve_half(0, LAM)
         Ms.append(eng.read_factors(0))
+        Ps.append(eng.debug_partials())
         eng.solve_half(1, LAM)
         Us.append(eng.read_factors(1))
+    nnz_padded = eng.block_stats(0)["nnz_padded"]
     eng.close()
     report = []
-    for name, reps in (("movie", Ms), ("user", Us)):
+    mblk = ds.shard_block(0)
+    slots = _split_slots(np.diff(mblk["row_ptr"]), nnz_padded)
+    sw = 45 * 64                                              # words per KP = 64 slot (44 + check word)
+    for name, reps_ in (("movie", Ms), ("user", Us)):
         side = 0 if name == "movie" else 1
-        rows = sorted(set(np.nonzero(np.any(reps[0] != reps[1], axis=1))[0].tolist())
-                      | set(np.nonzero(np.any(reps[0] != reps[2], axis=1))[0].tolist()))
+        rows = sorted(set().union(*[set(np.nonzero(np.any(reps_[0] != reps_[r], axis=1))[0].tolist())
+                                    for r in range(1, reps)]))
         if not rows:
             continue
-        blk = ds.shard_block(side)
-        opp = U0 if side == 0 else None
+        blk = mblk if side == 0 else ds.shard_block(side)
         for i in rows[:4]:
             lo, hi = int(blk["row_ptr"][i]), int(blk["row_ptr"][i + 1])
-            odd = [r for r in range(3) if sum(np.array_equal(reps[r][i], reps[q][i]) for q in range(3)) == 1]
-            err = []
-            if opp is not None:   # fp64 restatement of the movie update from U0 (MFeatureCalculator.java:82-99)
-                Y = opp[blk["col"][lo:hi], :64].astype(np.float64)
+            odd = [r for r in range(reps) if sum(np.array_equal(reps_[r][i], reps_[q][i]) for q in range(reps)) == 1]
+            err, where = [], ""
+            if side == 0:   # fp64 restatement of the movie update from U0 (MFeatureCalculator.java:82-99)
+                Y = U0[blk["col"][lo:hi], :64].astype(np.float64)
                 rr = blk["ratings"][lo:hi].astype(np.float64)
                 ref = np.linalg.solve(Y.T @ Y + np.float64(np.float32(LAM)) * (hi - lo) * np.eye(64), Y.T @ rr)
-                err = [float(np.max(np.abs(reps[r][i] - ref)) / np.max(np.abs(ref))) for r in range(3)]
-            report.append(f"{name} row {i} deg {hi - lo} deviating rep(s) {odd} fp64 err per rep {err}")
-    assert not report, f"{len(report)} nondeterministic rows: " + "; ".join(report)
+                err = [float(np.max(np.abs(reps_[r][i] - ref)) / np.max(np.abs(ref))) for r in range(reps)]
+                if i in slots:
+                    s0, s1 = slots[i]
+                    diff = [r for r in range(1, reps)
+                            if not np.array_equal(Ps[r][s0 * sw:s1 * sw], Ps[0][s0 * sw:s1 * sw])]
+                    where = (f" split row, slots [{s0},{s1}): partial slots differ from rep 0 in reps {diff}"
+                             if diff else f" split row, slots [{s0},{s1}): partial slots IDENTICAL in every rep")
+                else:
+                    where = " FULL row"
+            report.append(f"{name} row {i} deg {hi - lo}{where}; deviating rep(s) {odd}; fp64 err per rep {err}")
+        report.append(f"{name}: {len(rows)} differing rows in total")
+    assert not report, "nondeterministic rows: " + "; ".join(report)
 
 
 def test_engine_ordered_with_torch_default_stream(cfk):

@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Per-kernel register / spill / LDS / occupancy table of als_kernels.hip for gfx950 (compiler remarks).
+
+  python tools/resource_usage.py [extra hipcc flags...]
+"""
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "collaborative-filtering-kafka_amd", "csrc")
+
+
+def main():
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{ROOT}/include", f"-I{CSRC}",
+           "-c", os.path.join(CSRC, "als_kernels.hip"), "-o", "/tmp/resource_usage.o",
+           "-Rpass-analysis=kernel-resource-usage"] + sys.argv[1:]
+    out = subprocess.run(cmd, capture_output=True, text=True).stderr
+    rows, cur = [], None
+    for line in out.splitlines():
+        m = re.search(r"remark: (.+?): (.+?) \[-Rpass", line)
+        if not m:
+            continue
+        key, val = m.group(1).strip(), m.group(2).strip()
+        if key == "Function Name":
+            cur = {"name": subprocess.run(["c++filt"], input=val, capture_output=True, text=True).stdout.strip()}
+            rows.append(cur)
+        elif cur is not None:
+            cur[key] = val
+    cols = ["VGPRs", "AGPRs", "VGPRs Spill", "TotalSGPRs", "LDS Size [bytes/block]", "Occupancy [waves/SIMD]"]
+    print("  ".join(f"{c[:12]:>12}" for c in cols), " kernel")
+    for r in rows:
+        name = re.sub(r"cfk::\(anonymous namespace\)::", "", r["name"]).replace("(cfk::SolveArgs)", "")
+        print("  ".join(f"{r.get(c, '-'):>12}" for c in cols), "", name)
+
+
+if __name__ == "__main__":
+    main()
