@@ -376,6 +376,15 @@ __device__ __forceinline__ f32x4 mfma_k32(const u32x4& a, const u32x4& b, f32x4 
         static_for<0, CFK_DRAIN_NOPS>([&](auto) { asm volatile("s_nop 7"); }); \
         __builtin_amdgcn_sched_barrier(0);                                    \
     } while (0)
+// RHS of the on-the-fly split path: computed before its block's MFMA group and materialised there (1), or
+// after it (0). With 0 (and SLP-vectorised packed-fp32 VALU), LLVM deferred the RHS products into v_pk_mul /
+// v_pk_add_f32 chains next to the next block's MFMAs, and on gfx950 that intermittently lost ~1/3 of RHS
+// component 3 in lanes 48..63 of a wave (tools/split_diag.py: 5 of 5 captured failures had this signature;
+// 9 wrong movie rows in 300 Netflix-shape halves). Both this and building the kernels without SLP
+// vectorisation (Makefile) remove it (0 in 300 halves each).
+#ifndef CFK_RHS_EARLY
+#define CFK_RHS_EARLY 1
+#endif
 // The solve's v_mfma_f32_16x16x4_f32 groups get the same treatment when CFK_SOLVE_DRAIN is set.
 #ifndef CFK_SOLVE_DRAIN
 #define CFK_SOLVE_DRAIN 0
@@ -1044,6 +1053,14 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                         M[b][q] = m;
                         L[b][q] = l;
                     }
+                if constexpr (CFK_RHS_EARLY) {
+#pragma unroll
+                    for (int t = 0; t < B; ++t)
+#pragma unroll
+                        for (int c = 0; c < C; ++c) acc.rhs[c] += x.r[t >> 2][t & 3] * y[t][c];
+#pragma unroll
+                    for (int c = 0; c < C; ++c) pin(acc.rhs[c]);
+                }
                 // the operands are materialised above (pin: MachineSink ignores sched_barrier), so the MFMA group
                 // below contains no VALU that could overwrite an operand register of an MFMA in flight
                 __builtin_amdgcn_sched_barrier(0);
@@ -1068,10 +1085,12 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                         acc.g[tile_index<C>(b1, b2)] = t;
                     }
                 MFMA_DRAIN();
+                if constexpr (!CFK_RHS_EARLY) {
 #pragma unroll
-                for (int t = 0; t < B; ++t)
+                    for (int t = 0; t < B; ++t)
 #pragma unroll
-                    for (int c = 0; c < C; ++c) acc.rhs[c] += x.r[t >> 2][t & 3] * y[t][c];
+                        for (int c = 0; c < C; ++c) acc.rhs[c] += x.r[t >> 2][t & 3] * y[t][c];
+                }
             };
             // Two blocks per trip with ping-pong buffers (no register rotation): column indices are loaded two
             // blocks ahead of their gathers' use, gathers and ratings one block ahead of their MFMAs.

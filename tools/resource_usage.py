@@ -15,7 +15,7 @@ CSRC = os.path.join(ROOT, "collaborative-filtering-kafka_amd", "csrc")
 def main():
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{ROOT}/include", f"-I{CSRC}",
            "-c", os.path.join(CSRC, "als_kernels.hip"), "-o", "/tmp/resource_usage.o",
-           "-Rpass-analysis=kernel-resource-usage"] + sys.argv[1:]
+           "-Rpass-analysis=kernel-resource-usage", "-fno-slp-vectorize"] + sys.argv[1:]
     out = subprocess.run(cmd, capture_output=True, text=True).stderr
     rows, cur = [], None
     for line in out.splitlines():
