@@ -180,7 +180,46 @@ int als_dataset_load_netflix(const char* path, als_dataset** out) {
     FILE* f = fopen(path, "rb");
     if (!f) return report(fail(ALS_ERR_IO, "cannot open %s", path));
     std::unique_ptr<als_dataset> ds(new als_dataset());
-    std::vector<char> line(1 << 16);
+    // BufferedReader.readLine semantics: a line ends at "\n", "\r" or "\r\n" and may be of any length
+    // (NetflixDataFormatProducer.java:44); the file is streamed through a fixed buffer.
+    std::vector<char> buf(1 << 20);
+    size_t bpos = 0, blen = 0;
+    bool eof = false;
+    std::string line;
+    auto next_line = [&](std::string& out) -> bool {
+        out.clear();
+        bool any = false;
+        for (;;) {
+            if (bpos == blen) {
+                if (eof) return any;
+                blen = fread(buf.data(), 1, buf.size(), f);
+                bpos = 0;
+                if (blen == 0) {
+                    eof = true;
+                    return any;
+                }
+            }
+            any = true;
+            const char* b = buf.data() + bpos;
+            const char* e = buf.data() + blen;
+            const char* p = b;
+            while (p < e && *p != '\n' && *p != '\r') ++p;
+            out.append(b, p);
+            bpos += (size_t)(p - b);
+            if (p == e) continue;                        // line continues in the next buffer
+            const char term = *p;
+            ++bpos;
+            if (term == '\r') {                          // "\r\n" counts as one terminator
+                if (bpos == blen && !eof) {
+                    blen = fread(buf.data(), 1, buf.size(), f);
+                    bpos = 0;
+                    if (blen == 0) eof = true;
+                }
+                if (bpos < blen && buf[bpos] == '\n') ++bpos;
+            }
+            return true;
+        }
+    };
     int64_t current = -1;
     int64_t lineno = 0;
     auto parse_int = [](const char* b, const char* e, int64_t& v) -> bool {
@@ -201,10 +240,9 @@ int als_dataset_load_netflix(const char* path, als_dataset** out) {
         v = neg ? -x : x;
         return true;
     };
-    while (fgets(line.data(), (int)line.size(), f)) {
+    while (next_line(line)) {
         ++lineno;
-        size_t n = strlen(line.data());
-        while (n > 0 && (line[n - 1] == '\n' || line[n - 1] == '\r')) --n;   // BufferedReader.readLine
+        const size_t n = line.size();
         const char* b = line.data();
         const char* e = b + n;
         if (n > 0 && b[n - 1] == ':') {                                   // row.endsWith(":")

@@ -198,3 +198,20 @@ def test_shard_coo_is_arrival_order_of_the_in_blocks(cfk, tiny_path):
             assert np.array_equal(np.bincount(coo["rows"], minlength=csr["n_rows"]), np.diff(csr["row_ptr"]))
             assert np.array_equal(coo["cols"][order], csr["col"])
             assert np.array_equal(coo["ratings"][order], csr["ratings"])
+
+
+def test_loader_long_lines_and_line_terminators(cfk, oracle_mod, tmp_path):
+    """BufferedReader.readLine (NetflixDataFormatProducer.java:44): lines of any length (a rating line with a
+    200 KB date field, far beyond any fixed buffer), and "\\n", "\\r\\n" and a lone "\\r" all end a line. The
+    loader must read exactly what the oracle's universal-newline parse reads."""
+    long_date = "2005-09-06" + "x" * 200_000
+    text = ("1:\n6,3," + long_date + "\n7,4,2005-01-01\r\n8,5,2005-01-02\r2:\r\n6,1\n"
+            "9,2," + long_date + "\r7,5,2004-12-31")          # last line without a terminator
+    p = tmp_path / "long.txt"
+    p.write_bytes(text.encode())
+    ds = cfk.Dataset.load_netflix(str(p))
+    m, u, r = ds.ratings()
+    mo, uo, ro = oracle_mod.parse_netflix(str(p))
+    assert list(m) == list(mo) == [1, 1, 1, 2, 2, 2]
+    assert list(u) == list(uo) == [6, 7, 8, 6, 9, 7]
+    assert list(r) == list(ro) == [3, 4, 5, 1, 2, 5]
