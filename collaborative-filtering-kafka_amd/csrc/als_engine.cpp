@@ -875,6 +875,16 @@ int als_debug_copy_partials(als_engine* e, void* host_dst, int64_t max_bytes, in
     return ALS_OK;
 }
 
+int als_block_path(const als_engine* e, int side, int* gram_path, int* presplit, int64_t* chunk) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    const Block& b = e->blk[side];
+    if (gram_path) *gram_path = (int)e->path;
+    if (presplit) *presplit = b.presplit ? 1 : 0;
+    if (chunk) *chunk = b.set ? chunk_entries(b.nnz_padded) : 0;
+    return ALS_OK;
+}
+
 int als_block_stats(const als_engine* e, int side, int64_t* n_tasks, int64_t* n_reduce, int64_t* nnz_padded) {
     if (int r = check_engine(e)) return r;
     if (int r = check_side(side)) return r;

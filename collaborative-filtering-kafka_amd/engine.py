@@ -377,6 +377,12 @@ class ALSEngine:
         call("als_debug_copy_partials", self._h, out.ctypes.data_as(ctypes.c_void_p), n.value, ctypes.byref(n))
         return out
 
+    def block_path(self, side) -> dict:
+        """Gram variant of the side's block: gram_path ('valu' | 'mfma_f32' | 'mfma_split'), presplit, chunk."""
+        g, p, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
+        call("als_block_path", self._h, _side(side), ctypes.byref(g), ctypes.byref(p), ctypes.byref(c))
+        return {"gram_path": ("valu", "mfma_f32", "mfma_split")[g.value], "presplit": bool(p.value), "chunk": c.value}
+
     def block_stats(self, side):
         a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         call("als_block_stats", self._h, _side(side), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))

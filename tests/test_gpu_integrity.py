@@ -109,6 +109,7 @@ def test_extreme_short_ratings_every_path(cfk, oracle_mod, monkeypatch, k, presp
         ref = oracle_mod.update_side(rows, F, LAM, "f64")
         ref32 = oracle_mod.update_side(rows, F.astype(np.float32), LAM, "f32")
         eng = _engine(cfk, k, "f32", side, ds.shard_block(side), len(opp.ids), F.astype(np.float32))
+        assert not eng.block_path(side)["presplit"]          # |r| > 256: never the bf16 RHS operand
         eng.solve_half(side, LAM)
         got = eng.read_factors(side)
         eng.close()
@@ -123,6 +124,7 @@ def test_presplit_path_with_bf16_exact_extreme_ratings(cfk, oracle_mod):
     ref = oracle_mod.update_side(b.user, F, LAM, "f64")
     ref32 = oracle_mod.update_side(b.user, F.astype(np.float32), LAM, "f32")
     eng = _engine(cfk, 64, "f32", 1, ds.shard_block(1), len(b.movie.ids), F.astype(np.float32))
+    assert eng.block_path(1) == {"gram_path": "mfma_split", "presplit": True, "chunk": eng.block_path(1)["chunk"]}
     eng.solve_half(1, LAM)
     got = eng.read_factors(1)
     eng.close()

@@ -1,0 +1,130 @@
+#!/usr/bin/env python3
+"""gpurun_out/prof_<tag>/ (tools/profile_round.sh) -> profiles/<name>/ summaries + profiles/traffic.json.
+
+Writes:
+  kernel_stats.csv            rocprofv3 --stats of the 20-step bench run (as produced)
+  main_launch_summary.json    per half (movie / user main launch, reduce launch): calls, avg/min/max ms from the
+                              kernel trace -- the figure bench.py's HIP-event avg_launch_ms must agree with
+  pmc_summary.json            per half: FETCH_SIZE x2 + WRITE_SIZE bytes per launch (MI355X guide corrections:
+                              KiB -> B, FETCH doubled on gfx950), and the SQ counters of the full launch and of
+                              the Gram alone (ALS_DEBUG_SKIP_SOLVE=1): MFMA busy share, issue stalls, clock
+  bench_line.json             the bench.py line of the same call
+and profiles/traffic.json (read by bench.py: per_side HBM bytes per launch).
+Sides: the main solve kernel dispatch with the largest grid is the user half (480,189 tasks), the next the movie
+half (FULL + PARTIAL tasks); the REDUCE kernel instantiation is recognised by its last template argument.
+
+  python tools/prof_summary.py <tag> <profiles subdir>
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def is_reduce(name):
+    if "als_solve_mfma<" not in name:
+        return False
+    return name.split("als_solve_mfma<", 1)[1].split(">")[0].split(",")[-1].strip() == "true"
+
+
+def role_of(name, grid, grids):
+    if "als_solve" not in name:
+        return None
+    if is_reduce(name):
+        return "reduce"
+    big = sorted(grids, reverse=True)
+    if grid == big[0]:
+        return "user"
+    if len(big) > 1 and grid == big[1]:
+        return "movie"
+    return "other"
+
+
+def load_rows(pattern):
+    rows = []
+    for f in glob.glob(pattern, recursive=True):
+        rows += list(csv.DictReader(open(f)))
+    return rows
+
+
+def main(tag, name):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles", name)
+    os.makedirs(dst, exist_ok=True)
+    out = {}
+    # --- kernel trace ---
+    tr = load_rows(f"{src}/trace/**/*kernel_trace.csv")
+    st = glob.glob(f"{src}/trace/**/*kernel_stats.csv", recursive=True)
+    if st:
+        shutil.copy(st[0], os.path.join(dst, "kernel_stats.csv"))
+    grid = lambda r: int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)
+    grids = {grid(r) for r in tr if "als_solve" in r["Kernel_Name"] and not is_reduce(r["Kernel_Name"])}
+    dur = defaultdict(list)
+    for r in tr:
+        role = role_of(r["Kernel_Name"], grid(r), grids)
+        if role:
+            dur[role].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    out["trace"] = {k: {"calls": len(v), "avg_ms": sum(v) / len(v), "min_ms": min(v), "max_ms": max(v),
+                        "avg_ms_without_first": sum(v[1:]) / max(1, len(v) - 1)} for k, v in dur.items()}
+    json.dump({"source": f"prof_{tag}/trace", "launches": out["trace"]}, open(os.path.join(dst, "main_launch_summary.json"), "w"), indent=1)
+    # --- PMC passes ---
+    def per_role(pattern):
+        rows = load_rows(pattern)
+        g = {int(r["Grid_Size"]) for r in rows if "als_solve" in r["Kernel_Name"] and not is_reduce(r["Kernel_Name"])}
+        acc = defaultdict(lambda: defaultdict(list))
+        disp = defaultdict(lambda: defaultdict(float))
+        for r in rows:
+            role = role_of(r["Kernel_Name"], int(r["Grid_Size"]), g)
+            if role:
+                disp[(role, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+        for (role, _), cnt in disp.items():
+            for c, v in cnt.items():
+                acc[role][c].append(v)
+        return {role: {c: sum(v) / len(v) for c, v in cs.items()} for role, cs in acc.items()}
+    fetch = per_role(f"{src}/fetch/**/*counter_collection.csv")
+    write = per_role(f"{src}/write/**/*counter_collection.csv")
+    traffic = {}
+    for role in ("movie", "user", "reduce"):
+        if role in fetch and role in write:
+            traffic[role] = {"fetch_bytes_x2": fetch[role]["FETCH_SIZE"] * 1024 * 2,
+                             "write_bytes": write[role]["WRITE_SIZE"] * 1024}
+            traffic[role]["hbm_bytes"] = traffic[role]["fetch_bytes_x2"] + traffic[role]["write_bytes"]
+    out["traffic"] = traffic
+    for pas in ("sq", "sq_gram"):
+        sq = per_role(f"{src}/{pas}/**/*counter_collection.csv")
+        res = {}
+        for role, c in sq.items():
+            d = dict(c)
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "GRBM_GUI_ACTIVE" in c:
+                # MFMA busy cycles are summed over all SIMDs (1024); GRBM_GUI_ACTIVE over the 8 XCDs
+                d["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8 * 1024)
+            if "SQ_WAIT_INST_ANY" in c and "SQ_WAVE_CYCLES" in c:
+                d["wait_inst_any_frac"] = c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"]
+                d["wait_any_frac"] = c.get("SQ_WAIT_ANY", 0) / c["SQ_WAVE_CYCLES"]
+                d["active_inst_any_frac"] = c.get("SQ_ACTIVE_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
+            res[role] = d
+        out[pas] = res
+    json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
+    b = os.path.join(src, "bench.json")
+    if os.path.exists(b):
+        line = [l for l in open(b) if l.startswith("{")]
+        if line:
+            open(os.path.join(dst, "bench_line.json"), "w").write(line[-1])
+    bench = json.loads(open(os.path.join(dst, "bench_line.json")).read()) if os.path.exists(os.path.join(dst, "bench_line.json")) else {}
+    cfg = bench.get("config", {})
+    json.dump({"k": cfg.get("k", 64), "nnz": cfg.get("nnz", 100_000_000),
+               "per_side": {s: traffic[s]["hbm_bytes"] for s in ("movie", "user") if s in traffic},
+               "detail": traffic, "source": f"profiles/{name}",
+               "note": "per launch: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> B; Infinity-Cache hits "
+                       "are counted by these counters"}, open(os.path.join(ROOT, "profiles", "traffic.json"), "w"),
+              indent=1)
+    print(json.dumps({k: out[k] for k in ("trace", "traffic")}, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
