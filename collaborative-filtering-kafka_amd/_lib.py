@@ -27,6 +27,7 @@ F64 = 1
 _STATUS = {
     1: "ALS_ERR_INVALID_ARGUMENT", 2: "ALS_ERR_UNSUPPORTED", 3: "ALS_ERR_DEVICE", 4: "ALS_ERR_OUT_OF_MEMORY",
     5: "ALS_ERR_STATE", 6: "ALS_ERR_IO", 7: "ALS_ERR_PARSE", 8: "ALS_ERR_DATA", 9: "ALS_ERR_INTEGRITY",
+    10: "ALS_ERR_COMM",
 }
 
 
@@ -55,6 +56,7 @@ _ppv = ctypes.POINTER(ctypes.c_void_p)
 SIGNATURES = [
     ("als_abi_version", _i, []),
     ("als_last_error", ctypes.c_char_p, []),
+    ("als_device_count", _i, [ctypes.POINTER(ctypes.c_int)]),
     ("als_engine_create", _i, [_i, _i, _i, _ppv]),
     ("als_engine_destroy", _i, [_vp]),
     ("als_engine_set_stream", _i, [_vp, _vp]),
@@ -70,6 +72,14 @@ SIGNATURES = [
     ("als_solve_half", _i, [_vp, _i, _f]),
     ("als_set_chunks", _i, [_vp, _i, _i, _pi64]),
     ("als_solve_half_chunk", _i, [_vp, _i, _f, _i]),
+    ("als_comm_unique_id", _i, [_vp, _i]),
+    ("als_comm_init", _i, [_vp, _i, _i, _vp]),
+    ("als_comm_init_group", _i, [_ppv, _i]),
+    ("als_comm_info", _i, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    ("als_allgather_shard", _i, [_vp, _i, _i64, _i64, _i64]),
+    ("als_comm_group_start", _i, []),
+    ("als_comm_group_end", _i, []),
+    ("als_comm_wait", _i, [_vp]),
     ("als_predict", _i, [_vp, _pi64, _i64, _pi64, _i64, _pf]),
     ("als_sq_error", _i, [_vp, _i, _pd, _pi64]),
     ("als_synchronize", _i, [_vp]),

@@ -28,7 +28,7 @@ class ALSApp:
     def __init__(self, num_partitions: int, num_features: int, als_lambda: float, num_als_iterations: int,
                  num_movies: int | None = None, num_users: int | None = None, *, precision: str = "f32",
                  seed: int = 42, device: int = 0, rank: int = 0, world_size: int = 1, group=None,
-                 overlap_chunks: int = 4):
+                 overlap_chunks: int = 4, exchange: str = "torch"):
         self.NUM_PARTITIONS = num_partitions
         self.NUM_FEATURES = num_features
         self.ALS_LAMBDA = float(np.float32(als_lambda))     # Float.parseFloat (ALSAppRunner.java:19)
@@ -48,6 +48,12 @@ class ALSApp:
         # next one is solved (1 = one launch, then one all-gather)
         self.overlap_chunks = max(1, int(overlap_chunks))
         self.chunk_slots = None
+        # "torch": torch.distributed collectives on the factor tensors (backend "nccl" = RCCL); "native": the
+        # engine's own RCCL communicator through the C ABI (als_comm_init / als_allgather_shard), the path a
+        # JNI caller uses. The rendezvous (sharing the RCCL unique id) uses the torch process group either way.
+        if exchange not in ("torch", "native"):
+            raise ValueError("exchange must be 'torch' or 'native'")
+        self.exchange = exchange
 
     # -------------------------------------------------------------------------------------------------
     def setup(self, ds: Dataset, check_duplicates: bool = True, engine_factory=None,
@@ -97,6 +103,11 @@ class ALSApp:
             eng.set_chunks(SIDE_USER, bounds)
         u0 = ds.init_user_factors(self.NUM_FEATURES, self.seed, self.world)
         eng.write_factors(SIDE_USER, u0)
+        if self.exchange == "native" and self.world > 1:
+            import torch.distributed as dist
+            uid = [eng.comm_unique_id() if self.rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0, group=self.group)
+            eng.comm_init(self.world, self.rank, uid[0])
         self.engine = eng
         self.nnz_total = nnz
         return self
@@ -112,6 +123,9 @@ class ALSApp:
 
     def _allgather(self, side: int):
         if self.world == 1:
+            return
+        if self.exchange == "native":
+            self.engine.allgather_shard(side, self.info[side]["slots_per_shard"])
             return
         import torch.distributed as dist
         if not self._stream_ordered():
@@ -132,8 +146,13 @@ class ALSApp:
             self._allgather(SIDE_USER)
             return
         # chunk c's all-gather (RCCL stream, ordered after chunk c's solve) overlaps chunk c+1's solve
-        import torch.distributed as dist
         S = self.info[SIDE_USER]["slots_per_shard"]
+        if self.exchange == "native":
+            for c, (lo, hi) in enumerate(self.chunk_slots):
+                self.engine.solve_half_chunk(SIDE_USER, self.ALS_LAMBDA, c)
+                self.engine.allgather_shard(SIDE_USER, S, lo, hi)
+            return
+        import torch.distributed as dist
         U = self.engine.factors[SIDE_USER]
         works = []
         for c, (lo, hi) in enumerate(self.chunk_slots):

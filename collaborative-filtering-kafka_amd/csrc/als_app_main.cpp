@@ -1,13 +1,17 @@
-// als_app -- command-line replacement for ALSAppRunner (apps/ALSAppRunner.java:10-37) on one MI355X.
+// als_app -- command-line replacement for ALSAppRunner (apps/ALSAppRunner.java:10-37) on 1..G MI355X.
 //
 //   als_app NUM_PARTITIONS NUM_FEATURES LAMBDA NUM_ITERATIONS dataset NUM_MOVIES NUM_USERS
-//           [--precision f32|f64] [--seed S] [--device D] [--out DIR]
+//           [--precision f32|f64] [--seed S] [--gpus G] [--out DIR]
 //
 // Same 7 positional arguments (README.md:35); the extras are optional trailing flags. The run follows the
 // reference topology (ALSApp.java:52-184) bulk-synchronously: ingest (NetflixDataFormatProducer), in-blocks
 // (M/URatings2BlocksProcessor), U0 after the EOF barrier (UFeatureInitializer), N iterations of
-// MFeatureCalculator-i then UFeatureCalculator-i on the GPU, and FeatureCollector's prediction matrix written
+// MFeatureCalculator-i then UFeatureCalculator-i on the GPUs, and FeatureCollector's prediction matrix written
 // to ./predictions/prediction_matrix_<timestamp> in EJML dense-CSV layout.
+// NUM_PARTITIONS drives the sharding: G = the largest divisor of NUM_PARTITIONS that is <= the number of GPUs
+// (or --gpus), so that shard(id) = id % G = (id % NUM_PARTITIONS) % G (PureModStreamPartitioner.java:9-10).
+// One process drives the G engines (one per GPU); every half ends with an RCCL all-gather of each shard
+// (als_allgather_shard), the replacement for the per-iteration feature topics (ALSApp.java:105-151).
 // Deviations that turn reference hangs into errors: duplicate (user, movie) pairs, and NUM_MOVIES /
 // NUM_USERS not equal to the rated-entity counts (FeatureCollector.java:43 would never fire).
 #include <sys/stat.h>
@@ -20,6 +24,7 @@
 #include <cstring>
 #include <cmath>
 #include <ctime>
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -81,7 +86,7 @@ int main(int argc, char** argv) {
     const char* dataset = argv[5];
     int precision = ALS_F32;
     unsigned long long seed = 42;
-    int device = 0;
+    int gpus = 0;
     std::string outdir = "./predictions";
     for (int i = 8; i < argc; ++i) {
         std::string a = argv[i];
@@ -92,8 +97,8 @@ int main(int argc, char** argv) {
             else { fprintf(stderr, "als_app: --precision f32|f64\n"); return 1; }
         } else if (a == "--seed" && i + 1 < argc) {
             seed = strtoull(argv[++i], nullptr, 10);
-        } else if (a == "--device" && i + 1 < argc) {
-            device = atoi(argv[++i]);
+        } else if (a == "--gpus" && i + 1 < argc) {
+            gpus = atoi(argv[++i]);
         } else if (a == "--out" && i + 1 < argc) {
             outdir = argv[++i];
         } else {
@@ -101,6 +106,12 @@ int main(int argc, char** argv) {
             return 1;
         }
     }
+    int ndev = 0;
+    if (als_device_count(&ndev) != ALS_OK || ndev < 1) return die("no GPU");
+    const int cap = gpus > 0 ? std::min(gpus, ndev) : ndev;
+    int G = 1;
+    for (int g = 1; g <= cap; ++g)
+        if (P % g == 0) G = g;
 
     printf("Start at %s\n", java_timestamp().c_str());
     als_dataset* ds = nullptr;
@@ -120,62 +131,88 @@ int main(int argc, char** argv) {
                 (long long)NM, (long long)NU, (long long)nm, (long long)nu);
         return 1;
     }
-    printf("Got EOF: %lld ratings, %lld movies, %lld users (NUM_PARTITIONS=%lld; 1 GPU)\n", (long long)nnz,
-           (long long)nm, (long long)nu, P);
+    printf("Got EOF: %lld ratings, %lld movies, %lld users (NUM_PARTITIONS=%lld -> %d GPU shard%s)\n", (long long)nnz,
+           (long long)nm, (long long)nu, P, G, G > 1 ? "s" : "");
 
-    als_engine* e = nullptr;
-    if (als_engine_create(device, (int)K, precision, &e) != ALS_OK) return die("engine");
+    // One engine per GPU: shard g's in-blocks of both sides + full replicas of both factor matrices (slot order).
     const int k = (int)K;
-    for (int side = 0; side < 2; ++side) {
-        int64_t n_rows, row_off, bnnz, S, n_slots;
-        als_dataset_shard_info(ds, side, 1, 0, &n_rows, &row_off, &bnnz, &S, &n_slots);
-        std::vector<int64_t> rp(n_rows + 1);
-        std::vector<int32_t> col(bnnz);
-        std::vector<int16_t> rat(bnnz);
-        if (als_dataset_shard_block(ds, side, 1, 0, rp.data(), col.data(), rat.data(), nullptr) != ALS_OK)
-            return die("blocks");
-        int64_t n_opp = side == 0 ? nu : nm;
-        if (als_set_block(e, side, n_rows, row_off, n_opp, rp.data(), col.data(), rat.data()) != ALS_OK)
-            return die("set_block");
-        if (als_alloc_factors(e, side, n_slots) != ALS_OK) return die("alloc");
+    std::vector<als_engine*> eng(G, nullptr);
+    int64_t S[2] = {0, 0}, n_slots[2] = {0, 0};
+    for (int g = 0; g < G; ++g) {
+        if (als_engine_create(g, k, precision, &eng[g]) != ALS_OK) return die("engine");
+        for (int side = 0; side < 2; ++side) {
+            int64_t n_rows, row_off, bnnz, o_rows, o_off, o_nnz, o_S;
+            als_dataset_shard_info(ds, side, G, g, &n_rows, &row_off, &bnnz, &S[side], &n_slots[side]);
+            als_dataset_shard_info(ds, 1 - side, G, g, &o_rows, &o_off, &o_nnz, &o_S, &n_slots[1 - side]);
+            std::vector<int64_t> rp(n_rows + 1);
+            std::vector<int32_t> col(bnnz);
+            std::vector<int16_t> rat(bnnz);
+            if (als_dataset_shard_block(ds, side, G, g, rp.data(), col.data(), rat.data(), nullptr) != ALS_OK)
+                return die("blocks");
+            if (als_set_block(eng[g], side, n_rows, row_off, n_slots[1 - side], rp.data(), col.data(), rat.data()) !=
+                ALS_OK)
+                return die("set_block");
+            if (als_alloc_factors(eng[g], side, n_slots[side]) != ALS_OK) return die("alloc");
+        }
     }
-    std::vector<float> U0((size_t)nu * k);
-    if (als_dataset_init_user_factors(ds, k, seed, 1, U0.data(), k, nu) != ALS_OK) return die("init");
-    if (precision == ALS_F32) {
-        if (als_write_factors(e, ALS_SIDE_USER, 0, nu, U0.data(), k) != ALS_OK) return die("upload");
-    } else {
-        std::vector<double> u64(U0.begin(), U0.end());
-        if (als_write_factors(e, ALS_SIDE_USER, 0, nu, u64.data(), k) != ALS_OK) return die("upload");
+    // the communicator is created for G = 1 too, so a one-GPU run takes the same exchange path
+    if (als_comm_init_group(eng.data(), G) != ALS_OK) return die("RCCL communicator");
+    const int64_t nu_slots = n_slots[ALS_SIDE_USER];
+    std::vector<float> U0((size_t)nu_slots * k);
+    if (als_dataset_init_user_factors(ds, k, seed, G, U0.data(), k, nu_slots) != ALS_OK) return die("init");
+    std::vector<double> U0d;
+    if (precision == ALS_F64) U0d.assign(U0.begin(), U0.end());
+    for (int g = 0; g < G; ++g) {
+        const void* src = precision == ALS_F32 ? (const void*)U0.data() : (const void*)U0d.data();
+        if (als_write_factors(eng[g], ALS_SIDE_USER, 0, nu_slots, src, k) != ALS_OK) return die("upload");
     }
+    // One half = every engine's solve (asynchronous, one GPU each), then the grouped all-gather of every shard
+    // (MFeatureCalculator / UFeatureCalculator fan-out, MFeatureCalculator.java:106-132).
+    auto half = [&](int side) -> bool {
+        for (int g = 0; g < G; ++g)
+            if (als_solve_half(eng[g], side, lambda) != ALS_OK) return false;
+        if (als_comm_group_start() != ALS_OK) return false;
+        for (int g = 0; g < G; ++g)
+            if (als_allgather_shard(eng[g], side, S[side], 0, S[side]) != ALS_OK) return false;
+        return als_comm_group_end() == ALS_OK;
+    };
     struct timeval t0, t1;
     gettimeofday(&t0, nullptr);
     for (long long it = 0; it < N; ++it) {
-        if (als_solve_half(e, ALS_SIDE_MOVIE, lambda) != ALS_OK) return die("solve movies");
-        if (als_solve_half(e, ALS_SIDE_USER, lambda) != ALS_OK) return die("solve users");
+        if (!half(ALS_SIDE_MOVIE)) return die("movie half");
+        if (!half(ALS_SIDE_USER)) return die("user half");
     }
-    if (als_synchronize(e) != ALS_OK) return die("sync");
+    for (int g = 0; g < G; ++g)
+        if (als_synchronize(eng[g]) != ALS_OK) return die("sync");
     gettimeofday(&t1, nullptr);
     const double secs = (t1.tv_sec - t0.tv_sec) + 1e-6 * (t1.tv_usec - t0.tv_usec);
     double se = 0;
     int64_t cnt = 0;
-    if (als_sq_error(e, ALS_SIDE_MOVIE, &se, &cnt) != ALS_OK) return die("sq_error");
+    for (int g = 0; g < G; ++g) {
+        double s1 = 0;
+        int64_t c1 = 0;
+        if (als_sq_error(eng[g], ALS_SIDE_MOVIE, &s1, &c1) != ALS_OK) return die("sq_error");
+        se += s1;
+        cnt += c1;
+    }
     printf("ALS: %lld iterations in %.3f s (%.3e ratings/s per iteration); MSE %.6f RMSE %.6f\n", N, secs,
            N > 0 ? (double)nnz * N / secs : 0.0, cnt ? se / cnt : 0.0, cnt ? std::sqrt(se / cnt) : 0.0);
 
-    // FeatureCollector: factors in ascending id order (slot order for one shard); U M^T on the GPU with the
-    // collector's Java-float dot, then the EJML CSV text on the host.
+    // FeatureCollector: factors in ascending id order (their slots in engine 0's gathered replicas); U M^T on the
+    // GPU with the collector's Java-float dot, then the EJML CSV text on the host.
     printf("Start Prediction Matrix Computation at %s\n", java_timestamp().c_str());
     std::vector<int64_t> urows(nu), mrows(nm);
-    for (int64_t i = 0; i < nu; ++i) urows[i] = i;
-    for (int64_t i = 0; i < nm; ++i) mrows[i] = i;
+    if (als_dataset_slots(ds, ALS_SIDE_USER, G, urows.data()) != ALS_OK ||
+        als_dataset_slots(ds, ALS_SIDE_MOVIE, G, mrows.data()) != ALS_OK)
+        return die("slots");
     std::vector<float> pred((size_t)nu * (size_t)nm);
-    if (als_predict(e, urows.data(), nu, mrows.data(), nm, pred.data()) != ALS_OK) return die("predict");
+    if (als_predict(eng[0], urows.data(), nu, mrows.data(), nm, pred.data()) != ALS_OK) return die("predict");
     mkdir(outdir.c_str(), 0755);
     const std::string path = outdir + "/prediction_matrix_" + java_timestamp();
     printf("Done at %s\n", java_timestamp().c_str());
     if (als_write_prediction_matrix_csv(path.c_str(), pred.data(), nu, nm) != ALS_OK) return die("csv");
     printf("Prediction matrix: %s\n", path.c_str());
-    als_engine_destroy(e);
+    for (auto* e : eng) als_engine_destroy(e);
     als_dataset_destroy(ds);
     return 0;
 }

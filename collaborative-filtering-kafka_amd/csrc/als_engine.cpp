@@ -2,6 +2,7 @@
 // buffers, and the half-iteration launch. See include/als.h for the reference interface each entry
 // point replaces.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdarg>
@@ -96,6 +97,12 @@ struct als_engine {
                                     // integrity check: every slot then reads as written by another launch)
     bool debug_fixed_gen = false;   // ALS_DEBUG_FIXED_GEN=1: every launch uses generation 1, so partial slots of
                                     // repeated launches are bitwise comparable (als_debug_copy_partials)
+    ncclComm_t comm = nullptr;      // RCCL communicator over the G engines (one per GPU) of a sharded run
+    int world = 1, rank = 0;
+    hipStream_t comm_stream = nullptr;   // all-gathers run here, overlapping the next chunk's solve
+    hipEvent_t solved = nullptr;         // recorded on `stream` before each all-gather
+    hipEvent_t gathered[2] = {nullptr, nullptr};   // last all-gather of each side, on comm_stream
+    bool gather_pending[2] = {false, false};
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     std::vector<TimingRec> pending;
@@ -112,7 +119,19 @@ int check_engine(const als_engine* e) {
 // Drain the engine's stream and read the partial-slot integrity record (cfk::SlotCodec): a REDUCE task that
 // found a slot it could not see freshly written by this launch's PARTIAL task makes every later synchronising
 // call fail until als_integrity_status(..., reset = 1).
+// Order the engine's stream after the pending all-gathers of the given sides (comm_stream -> stream).
+int wait_gathers(als_engine* e, bool movie, bool user) {
+    const bool want[2] = {movie, user};
+    for (int s = 0; s < 2; ++s)
+        if (want[s] && e->gather_pending[s]) {
+            HIP_TRY(hipStreamWaitEvent(e->stream, e->gathered[s], 0));
+            e->gather_pending[s] = false;
+        }
+    return ALS_OK;
+}
+
 int sync_checked(als_engine* e) {
+    if (int r = wait_gathers(e, true, true)) return r;
     HIP_TRY(hipStreamSynchronize(e->stream));
     uint32_t rec[cfk::INTEGRITY_WORDS];
     HIP_TRY(hipMemcpy(rec, e->d_integrity, sizeof(rec), hipMemcpyDeviceToHost));
@@ -162,6 +181,13 @@ int64_t chunk_entries(int64_t nnz_padded) {
 extern "C" {
 
 int als_abi_version(void) { return ALS_ABI_VERSION; }
+
+int als_device_count(int* n) {
+    if (!n) return fail(ALS_ERR_INVALID_ARGUMENT, "n is NULL");
+    *n = 0;
+    HIP_TRY(hipGetDeviceCount(n));
+    return ALS_OK;
+}
 const char* als_last_error(void) { return g_last_error.c_str(); }
 
 int als_engine_create(int device, int num_features, int precision, als_engine** out) {
@@ -234,6 +260,11 @@ int als_engine_destroy(als_engine* e) {
     for (auto& rec : e->pending)
         for (auto ev : rec.ev) (void)hipEventDestroy(ev);
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
+    if (e->comm_stream) (void)hipStreamSynchronize(e->comm_stream);
+    if (e->comm) (void)ncclCommDestroy(e->comm);
+    if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
+    for (auto ev : {e->solved, e->gathered[0], e->gathered[1]})
+        if (ev) (void)hipEventDestroy(ev);
     if (e->own_stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return ALS_OK;
@@ -562,6 +593,7 @@ int als_write_factors(als_engine* e, int side, int64_t row0, int64_t n_rows, con
     if (n_rows == 0) return ALS_OK;
     if (!host_src) return fail(ALS_ERR_INVALID_ARGUMENT, "host_src is NULL");
     HIP_TRY(hipSetDevice(e->device));
+    if (int r = wait_gathers(e, true, true)) return r;
     const size_t es = e->elem();
     // Rows are packed kp wide (padding columns zero) into pinned staging and written by a copy kernel
     // (cfk::launch_upload) on the engine's stream: see copy16 in als_kernels.hip.
@@ -618,7 +650,7 @@ namespace {
 
 // One half (or one chunk of it): the FULL + PARTIAL launch, then the REDUCE launch.
 int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_t n_tasks, const Task* reduce,
-                int32_t n_reduce) {
+                int32_t n_reduce, bool first_chunk) {
     Block& b = e->blk[side];
     const Factors& self = e->fac[side];
     const Factors& opp = e->fac[1 - side];
@@ -631,6 +663,9 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
                     (long long)b.n_opp_rows, (long long)opp.n_rows);
     if (!(lambda >= 0.f)) return fail(ALS_ERR_INVALID_ARGUMENT, "lambda must be >= 0");
     HIP_TRY(hipSetDevice(e->device));
+    // the solve reads the opposite replica: wait for its all-gather; a whole half / first chunk also rewrites
+    // this side's rows, which an earlier all-gather of this side may still be sending
+    if (int r = wait_gathers(e, side == ALS_SIDE_USER || first_chunk, side == ALS_SIDE_MOVIE || first_chunk)) return r;
     cfk::SolveArgs a{};
     a.tasks = tasks;
     a.n_tasks = n_tasks;
@@ -685,7 +720,7 @@ int als_solve_half(als_engine* e, int side, float lambda) {
     if (int r = check_side(side)) return r;
     Block& b = e->blk[side];
     if (!b.set) return fail(ALS_ERR_STATE, "als_solve_half: no block set for side %d", side);
-    return launch_half(e, side, lambda, b.d_tasks, b.n_tasks, b.d_reduce, b.n_reduce);
+    return launch_half(e, side, lambda, b.d_tasks, b.n_tasks, b.d_reduce, b.n_reduce, true);
 }
 
 int als_set_chunks(als_engine* e, int side, int n_chunks, const int64_t* row_bounds) {
@@ -739,7 +774,7 @@ int als_solve_half_chunk(als_engine* e, int side, float lambda, int chunk) {
     if (chunk < 0 || chunk + 1 >= (int)b.coff.size())
         return fail(ALS_ERR_INVALID_ARGUMENT, "chunk %d out of range (%d chunks)", chunk, (int)b.coff.size() - 1);
     return launch_half(e, side, lambda, b.d_ctasks + b.coff[chunk], b.coff[chunk + 1] - b.coff[chunk],
-                       b.d_creduce + b.croff[chunk], b.croff[chunk + 1] - b.croff[chunk]);
+                       b.d_creduce + b.croff[chunk], b.croff[chunk + 1] - b.croff[chunk], chunk == 0);
 }
 
 int als_predict(als_engine* e, const int64_t* user_rows, int64_t n_users, const int64_t* movie_rows,
@@ -757,6 +792,7 @@ int als_predict(als_engine* e, const int64_t* user_rows, int64_t n_users, const 
         if (movie_rows[i] < 0 || movie_rows[i] >= M.n_rows) return fail(ALS_ERR_INVALID_ARGUMENT, "movie row out of range");
     if ((n_users + 15) / 16 > 65535) return fail(ALS_ERR_UNSUPPORTED, "at most 1,048,560 users per call (call per user range)");
     HIP_TRY(hipSetDevice(e->device));
+    if (int r = wait_gathers(e, true, true)) return r;
     int64_t *d_u = nullptr, *d_m = nullptr;
     float* d_out = nullptr;
     const size_t ob = (size_t)n_users * (size_t)n_movies * sizeof(float);
@@ -792,6 +828,7 @@ int als_sq_error(als_engine* e, int side, double* sum_sq_error, int64_t* count) 
     const Factors& opp = e->fac[1 - side];
     if (!self.ptr || !opp.ptr) return fail(ALS_ERR_STATE, "als_sq_error: factor matrices not allocated/bound");
     HIP_TRY(hipSetDevice(e->device));
+    if (int r = wait_gathers(e, true, true)) return r;
     cfk::SqErrArgs a{};
     a.tasks = b.d_tasks;
     a.n_tasks = b.n_tasks;
@@ -873,6 +910,127 @@ int als_debug_copy_partials(als_engine* e, void* host_dst, int64_t max_bytes, in
     if (bytes) *bytes = (int64_t)e->partial_bytes;
     if (host_dst && n > 0) HIP_TRY(hipMemcpy(host_dst, e->d_partials, (size_t)n, hipMemcpyDeviceToHost));
     return ALS_OK;
+}
+
+// ---- multi-GPU exchange (RCCL over xGMI) ---------------------------------------------------------------
+#define NCCL_TRY(expr)                                                                                     \
+    do {                                                                                                   \
+        ncclResult_t _r = (expr);                                                                          \
+        if (_r != ncclSuccess)                                                                             \
+            return fail(ALS_ERR_COMM, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(_r), __FILE__,     \
+                        __LINE__);                                                                         \
+    } while (0)
+
+static int comm_streams(als_engine* e) {
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&e->solved, hipEventDisableTiming));
+    for (auto& ev : e->gathered) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    return ALS_OK;
+}
+
+int als_comm_unique_id(void* id_out, int nbytes) {
+    if (!id_out || nbytes < (int)sizeof(ncclUniqueId))
+        return fail(ALS_ERR_INVALID_ARGUMENT, "unique id buffer must hold %d bytes", (int)sizeof(ncclUniqueId));
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    std::memcpy(id_out, &id, sizeof(id));
+    return ALS_OK;
+}
+
+int als_comm_init(als_engine* e, int world, int rank, const void* unique_id) {
+    if (int r = check_engine(e)) return r;
+    if (world < 1 || rank < 0 || rank >= world || !unique_id)
+        return fail(ALS_ERR_INVALID_ARGUMENT, "bad world/rank/unique_id (world %d, rank %d)", world, rank);
+    if (e->comm) return fail(ALS_ERR_STATE, "engine already has a communicator");
+    HIP_TRY(hipSetDevice(e->device));
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof(id));
+    NCCL_TRY(ncclCommInitRank(&e->comm, world, id, rank));
+    e->world = world;
+    e->rank = rank;
+    return comm_streams(e);
+}
+
+int als_comm_init_group(als_engine** engines, int n) {
+    if (!engines || n < 1) return fail(ALS_ERR_INVALID_ARGUMENT, "need >= 1 engines");
+    std::vector<int> devs(n);
+    for (int i = 0; i < n; ++i) {
+        if (int r = check_engine(engines[i])) return r;
+        if (engines[i]->comm) return fail(ALS_ERR_STATE, "engine %d already has a communicator", i);
+        devs[i] = engines[i]->device;
+        for (int j = 0; j < i; ++j)
+            if (devs[j] == devs[i]) return fail(ALS_ERR_INVALID_ARGUMENT, "engines %d and %d share device %d", j, i, devs[i]);
+    }
+    std::vector<ncclComm_t> comms(n);
+    NCCL_TRY(ncclCommInitAll(comms.data(), n, devs.data()));
+    for (int i = 0; i < n; ++i) {
+        engines[i]->comm = comms[i];
+        engines[i]->world = n;
+        engines[i]->rank = i;
+        if (int r = comm_streams(engines[i])) return r;
+    }
+    return ALS_OK;
+}
+
+int als_comm_info(const als_engine* e, int* world, int* rank) {
+    if (int r = check_engine(e)) return r;
+    if (world) *world = e->world;
+    if (rank) *rank = e->rank;
+    return ALS_OK;
+}
+
+int als_comm_group_start(void) {
+    NCCL_TRY(ncclGroupStart());
+    return ALS_OK;
+}
+
+int als_comm_group_end(void) {
+    NCCL_TRY(ncclGroupEnd());
+    return ALS_OK;
+}
+
+int als_allgather_shard(als_engine* e, int side, int64_t slots_per_shard, int64_t slot_lo, int64_t slot_hi) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    if (e->world == 1 && !e->comm) return ALS_OK;   // one shard: the replica is the matrix
+    if (!e->comm) return fail(ALS_ERR_STATE, "als_allgather_shard: no communicator (als_comm_init)");
+    const Factors& f = e->fac[side];
+    if (!f.ptr) return fail(ALS_ERR_STATE, "factors of side %d not allocated/bound", side);
+    const int64_t S = slots_per_shard;
+    if (S < 0 || slot_lo < 0 || slot_lo > slot_hi || slot_hi > S || S * e->world > f.n_rows)
+        return fail(ALS_ERR_INVALID_ARGUMENT, "slot range [%lld, %lld) of %lld slots per shard x %d shards vs %lld rows",
+                    (long long)slot_lo, (long long)slot_hi, (long long)S, e->world, (long long)f.n_rows);
+    if (slot_hi == slot_lo) return ALS_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    // after this engine's solve (stream) on comm_stream; the next solve that reads this side waits for it
+    HIP_TRY(hipEventRecord(e->solved, e->stream));
+    HIP_TRY(hipStreamWaitEvent(e->comm_stream, e->solved, 0));
+    const ncclDataType_t dt = e->precision == ALS_F64 ? ncclFloat64 : ncclFloat32;
+    const size_t row = (size_t)e->kp * e->elem();
+    char* base = (char*)f.ptr;
+    const size_t count = (size_t)(slot_hi - slot_lo) * e->kp;
+    if (slot_lo == 0 && slot_hi == S) {
+        // shard-major slots: the all-gather of equal S-row shards IS the whole matrix (in place)
+        NCCL_TRY(ncclAllGather(base + (size_t)e->rank * S * row, base, count, dt, e->comm, e->comm_stream));
+    } else {
+        // rows [lo, hi) of every shard: one in-place broadcast per shard owner, grouped
+        NCCL_TRY(ncclGroupStart());
+        for (int g = 0; g < e->world; ++g) {
+            char* p = base + ((size_t)g * S + slot_lo) * row;
+            NCCL_TRY(ncclBroadcast(p, p, count, dt, g, e->comm, e->comm_stream));
+        }
+        NCCL_TRY(ncclGroupEnd());
+    }
+    HIP_TRY(hipEventRecord(e->gathered[side], e->comm_stream));
+    e->gather_pending[side] = true;
+    return ALS_OK;
+}
+
+int als_comm_wait(als_engine* e) {
+    if (int r = check_engine(e)) return r;
+    HIP_TRY(hipSetDevice(e->device));
+    return wait_gathers(e, true, true);
 }
 
 int als_block_path(const als_engine* e, int side, int* gram_path, int* presplit, int64_t* chunk) {

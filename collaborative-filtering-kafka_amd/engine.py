@@ -337,6 +337,36 @@ class ALSEngine:
     def solve_half_chunk(self, side, lam: float, chunk: int):
         call("als_solve_half_chunk", self._h, _side(side), float(np.float32(lam)), int(chunk))
 
+    # -- multi-GPU exchange through the C ABI (RCCL over xGMI, als.h) -------------------------------------
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        call("als_comm_unique_id", buf, 128)
+        return buf.raw
+
+    def comm_init(self, world: int, rank: int, unique_id: bytes):
+        buf = ctypes.create_string_buffer(bytes(unique_id), 128)
+        call("als_comm_init", self._h, world, rank, buf)
+
+    @staticmethod
+    def comm_init_group(engines: list["ALSEngine"]):
+        """One process driving len(engines) GPUs (one engine per device)."""
+        arr = (ctypes.c_void_p * len(engines))(*[e._h.value for e in engines])
+        call("als_comm_init_group", arr, len(engines))
+
+    def comm_info(self) -> tuple[int, int]:
+        w, r = ctypes.c_int(), ctypes.c_int()
+        call("als_comm_info", self._h, ctypes.byref(w), ctypes.byref(r))
+        return w.value, r.value
+
+    def allgather_shard(self, side, slots_per_shard: int, slot_lo: int = 0, slot_hi: int | None = None):
+        """All-gather slots [slot_lo, slot_hi) of every shard of `side` into this engine's replica."""
+        hi = slots_per_shard if slot_hi is None else slot_hi
+        call("als_allgather_shard", self._h, _side(side), slots_per_shard, slot_lo, hi)
+
+    def comm_wait(self):
+        call("als_comm_wait", self._h)
+
     def predict(self, user_rows, movie_rows) -> np.ndarray:
         """FeatureCollector's U M^T (Java-float dots) for the given factor rows, on the GPU."""
         ur = np.ascontiguousarray(user_rows, np.int64)

@@ -43,8 +43,9 @@ typedef enum {
     ALS_ERR_IO = 6,
     ALS_ERR_PARSE = 7,
     ALS_ERR_DATA = 8,          /* input that hangs the reference (duplicate pair, count mismatch) */
-    ALS_ERR_INTEGRITY = 9      /* a split row's REDUCE task read a partial slot this launch had not written
+    ALS_ERR_INTEGRITY = 9,     /* a split row's REDUCE task read a partial slot this launch had not written
                                   (als_integrity_status); the results of that half are not trustworthy */
+    ALS_ERR_COMM = 10          /* RCCL error (als_comm_*, als_allgather_shard) */
 } als_status;
 
 typedef enum { ALS_SIDE_MOVIE = 0, ALS_SIDE_USER = 1 } als_side;
@@ -55,6 +56,7 @@ typedef struct als_engine als_engine;
 /* ---- version / errors --------------------------------------------------------------------------- */
 int         als_abi_version(void);
 const char* als_last_error(void);
+int         als_device_count(int* n);
 
 /* ---- engine lifetime ---------------------------------------------------------------------------- */
 /* Replaces the per-task processor state of MFeatureCalculator/UFeatureCalculator.init (:29-46).
@@ -117,6 +119,29 @@ int als_solve_half(als_engine* e, int side, float lambda);
  * (ALSApp.java:105-148) overlapped with compute. Replaces any previous chunking of that side. */
 int als_set_chunks(als_engine* e, int side, int n_chunks, const int64_t* row_bounds);
 int als_solve_half_chunk(als_engine* e, int side, float lambda, int chunk);
+
+/* ---- multi-GPU: shards + RCCL all-gather over xGMI ------------------------------------------------
+ * Replaces the per-iteration feature topics (ALSApp.java:105-151): entities are sharded by raw id % G
+ * (PureModStreamPartitioner.java:9-10) into shard-major slots (slot = shard * S + rank in shard, S = slots per
+ * shard), every engine holds its shard's in-blocks and a full replica of both factor matrices, and each half
+ * ends with one all-gather of the updated shard. One engine per GPU; either one process per GPU (unique id from
+ * als_comm_unique_id on one process, shared by the caller, then als_comm_init on every process) or one process
+ * driving G GPUs (als_comm_init_group). The exchange is enqueued on the engine's stream after its solve. */
+int als_comm_unique_id(void* id_out, int nbytes);   /* nbytes >= 128 */
+int als_comm_init(als_engine* e, int world, int rank, const void* unique_id);
+int als_comm_init_group(als_engine** engines, int n);
+int als_comm_info(const als_engine* e, int* world, int* rank);
+/* Gather slots [slot_lo, slot_hi) of every shard of `side` (all of them: slot_lo = 0, slot_hi = S) into every
+ * engine's replica. A single host thread driving several engines wraps its per-engine calls in
+ * als_comm_group_start / als_comm_group_end. A no-op for an engine without a communicator (G = 1). */
+int als_allgather_shard(als_engine* e, int side, int64_t slots_per_shard, int64_t slot_lo, int64_t slot_hi);
+int als_comm_group_start(void);
+int als_comm_group_end(void);
+/* The all-gathers run on the engine's own communication stream, after the solve that produced the shard and
+ * overlapping any later solve that does not depend on them (e.g. the next user-half chunk); the engine orders
+ * its next solve of the other side, and every synchronising call, after them. Work issued by the caller on
+ * the engine's stream that reads the gathered replicas (e.g. torch ops) must call als_comm_wait first. */
+int als_comm_wait(als_engine* e);
 
 /* FeatureCollector's prediction matrix (FeatureCollector.java:90-101) from the resident factors:
  * host_out[u * n_movies + m] = U[user_rows[u]] . M[movie_rows[m]] as a Java float dot (fp32 products and

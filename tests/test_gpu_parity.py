@@ -439,3 +439,51 @@ def test_engine_ordered_with_torch_default_stream(cfk):
     eng.close()
     assert np.abs(M).sum() > 0
     assert np.array_equal(seen, M), int(np.any(seen != M, axis=1).sum())
+
+
+def test_native_rccl_exchange_world1(cfk, oracle_mod):
+    """The C-ABI exchange (als_comm_unique_id / als_comm_init / als_allgather_shard, RCCL) on a one-rank
+    communicator: the all-gather of whole shards and of slot ranges leaves the replicas bitwise unchanged, and
+    the chunked user half with an all-gather after every chunk (on the engine's comm stream, overlapping the
+    next chunk) reproduces als_solve_half exactly. The N > 1 exchange runs on the driver's multi-GPU node."""
+    ds, b = _synthetic(cfk, oracle_mod)
+    eng = cfk.ALSEngine(64, "f32")
+    uid = cfk.ALSEngine.comm_unique_id()
+    assert len(uid) == 128
+    eng.comm_init(1, 0, uid)
+    assert eng.comm_info() == (1, 0)
+    info = [ds.shard_info(s) for s in (0, 1)]
+    for side in (0, 1):
+        c = ds.shard_coo(side)
+        eng.alloc_factors(side, info[side]["n_slots"])
+        eng.set_block_coo(side, c["n_rows"], c["rows"], c["cols"], c["ratings"], 0, info[1 - side]["n_slots"])
+    eng.write_factors(1, ds.init_user_factors(64, 3))
+    eng.solve_half(0, LAM)
+    M = eng.read_factors(0)
+    eng.allgather_shard(0, info[0]["slots_per_shard"])
+    eng.allgather_shard(0, info[0]["slots_per_shard"], 5, 17)
+    assert np.array_equal(eng.read_factors(0), M)
+    eng.solve_half(1, LAM)
+    U = eng.read_factors(1)
+    n = info[1]["n_rows"]
+    bounds = [0, n // 3, 2 * n // 3, n]
+    eng.set_chunks(1, bounds)
+    for c in range(3):
+        eng.solve_half_chunk(1, LAM, c)
+        eng.allgather_shard(1, info[1]["slots_per_shard"], bounds[c], bounds[c + 1])
+    assert np.array_equal(eng.read_factors(1), U)
+    eng.solve_half(0, LAM)             # reads U: ordered after the pending all-gathers of the user side
+    M2 = eng.read_factors(0)
+    eng.close()
+    ref = oracle_mod.update_side(b.movie, U.astype(np.float64), LAM, "f64")
+    assert np.linalg.norm(M2 - ref) / np.linalg.norm(ref) < 1e-4
+
+
+def test_comm_init_group_one_engine(cfk):
+    e = cfk.ALSEngine(16, "f32")
+    cfk.ALSEngine.comm_init_group([e])
+    assert e.comm_info() == (1, 0)
+    from cfk_amd._lib import ALSError
+    with pytest.raises(ALSError, match="ALS_ERR_STATE"):
+        cfk.ALSEngine.comm_init_group([e])            # already has a communicator
+    e.close()
