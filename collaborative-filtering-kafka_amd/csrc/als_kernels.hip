@@ -459,6 +459,21 @@ __device__ __forceinline__ float col_bcast(float v) {
     const int addr = ((int)(__lane_id() & 15) + 16 * G) * 4;
     return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
 }
+// the same broadcast with two VALU lane swaps (v_permlane16_swap: even/odd row of each pair; v_permlane32_swap:
+// low/high pair), no LDS round trip: shorter latency, but both operands are rewritten (register copies)
+template <int G>
+__device__ __forceinline__ float col_bcast_swap(float v) {
+    const auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+    const int w = (int)s16[G & 1];
+    const auto s32 = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+    return __int_as_float((int)s32[G >> 1]);
+}
+// CFK_COL_SWAP: sweep column broadcasts by lane swaps for KP >= this (one wave per SIMD at KP = 128, where the
+// pivot chain's latency is exposed), by ds_bpermute below it
+#ifndef CFK_COL_SWAP
+#define CFK_COL_SWAP 1000
+#endif
+
 // sum over the 4 rows at each column, result in every row
 __device__ __forceinline__ float col_sum(float v) {
     const int x = __float_as_int(v);
@@ -484,6 +499,7 @@ __device__ __forceinline__ float row_sum_to_last(float v) {
 // a[i][p] + a[i][p] (d - 1)(-1/d) = a[i][p] / d. That FMA is accurate to a few ulp only while d <= 1,
 // which the caller guarantees by Jacobi-scaling the system to a unit diagonal (every later pivot is a
 // Schur-complement diagonal of a unit-diagonal SPD matrix, so it stays in (0, 1]).
+template <bool SWAP>
 __device__ __forceinline__ void sweep_tile(f32x4& a, int lane) {
     static_for<0, 16>([&](auto P_) {
         constexpr int p = decltype(P_)::value;
@@ -491,7 +507,7 @@ __device__ __forceinline__ void sweep_tile(f32x4& a, int lane) {
         const float nrd = __builtin_amdgcn_rcpf(-bcast(a[pr], 16 * pg + p));   // -1 / d
         const bool piv = lane == 16 * pg + p;   // 16 lane masks, CSE-d across the 4 diagonal tiles (SGPRs)
         a[pr] = piv ? a[pr] - 1.f : a[pr];
-        const float t = col_bcast<pg>(a[pr]) * nrd;                   // a[p][c] (d - 1 at c = p) * (-1/d)
+        const float t = (SWAP ? col_bcast_swap<pg>(a[pr]) : col_bcast<pg>(a[pr])) * nrd;   // a[p][c] (d - 1 at c = p) * (-1/d)
         f32x4 cp;
 #pragma unroll
         for (int r = 0; r < 4; ++r) cp[r] = row_lane_bcast<p>(a[r]);   // a[4g + r][p] (d - 1 at row p)
@@ -620,7 +636,7 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
     static_for<0, C>([&](auto P_) {
         constexpr int P = decltype(P_)::value;
         f32x4 S = T.get(tile_index<C>(P, P));
-        sweep_tile(S, lane);
+        sweep_tile<(16 * C >= CFK_COL_SWAP)>(S, lane);
         T.put(tile_index<C>(P, P), S);
         // Block columns J in DESCENDING order: V'_PJ only updates T_IJ (P < I <= J) from the still-unreplaced
         // T_PI (I <= J), so block row P can take V'_PJ right away and one V is live at a time. Every T_IJ
