@@ -54,6 +54,14 @@ struct Block {
     Task* d_ctasks = nullptr;       // chunk-major FULL + PARTIAL tasks (LPT inside each chunk)
     Task* d_creduce = nullptr;      // chunk-major REDUCE tasks
     std::vector<int32_t> coff, croff;   // chunk c = d_ctasks[coff[c], coff[c+1]), d_creduce[croff[c], ...)
+    // short rows solved in entry space (cfk::launch_dual), by entry-tile count cd = 2 (1 block) / 4 (2 blocks)
+    Task* d_dual[2] = {nullptr, nullptr};
+    int32_t n_dual[2] = {0, 0};
+    std::vector<Task> h_dual[2];
+    Task* d_cdual[2] = {nullptr, nullptr};
+    std::vector<int32_t> cdoff[2];
+    Task* d_sq_tasks = nullptr;     // every FULL + PARTIAL task incl. the short rows (als_sq_error)
+    int32_t n_sq = 0;
     bool presplit = false;          // gather a pre-split (bf16 h/m/l) copy of the opposite table
 };
 
@@ -156,6 +164,11 @@ void free_block(Block& b) {
     (void)hipFree(b.d_task_se);
     (void)hipFree(b.d_ctasks);
     (void)hipFree(b.d_creduce);
+    for (int c = 0; c < 2; ++c) {
+        (void)hipFree(b.d_dual[c]);
+        (void)hipFree(b.d_cdual[c]);
+    }
+    (void)hipFree(b.d_sq_tasks);
     b = Block();
 }
 
@@ -382,6 +395,24 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
             reduce.push_back(r);
         }
     }
+    // Short rows in entry space (split-bf16 path): rows of <= 2 blocks at KP = 128, 1 block at KP = 64 solve the
+    // (padded entries)^2 system of als_solve_dual instead of the KP x KP one. ALS_DUAL=0 turns it off.
+    std::vector<Task> sq_all = tasks;
+    std::vector<Task> dual[2];
+    {
+        const int max_cd = e->path != Path::MFMA_SPLIT ? 0 : e->kp == 128 ? 4 : e->kp == 64 ? 2 : 0;
+        bool on = max_cd > 0;
+        if (const char* env = getenv("ALS_DUAL")) on = on && env[0] != '0';
+        if (on) {
+            std::vector<Task> keep;
+            for (const Task& t : tasks) {
+                const int cd = 2 * ((t.nent + cfk::BLOCK_ENTRIES - 1) / cfk::BLOCK_ENTRIES);
+                if (t.kind == cfk::TASK_FULL && t.ndeg > 0 && cd <= max_cd) dual[cd == 2 ? 0 : 1].push_back(t);
+                else keep.push_back(t);
+            }
+            tasks.swap(keep);
+        }
+    }
     if (slots > INT32_MAX || tasks.size() > (size_t)INT32_MAX) {
         drop();
         return fail(ALS_ERR_UNSUPPORTED, "too many tasks / partial slots");
@@ -389,6 +420,8 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     // Longest tasks first (LPT): the grid drains with a short tail.
     std::stable_sort(tasks.begin(), tasks.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
     std::stable_sort(reduce.begin(), reduce.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
+    for (auto& d : dual)
+        std::stable_sort(d.begin(), d.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
 
     hipError_t st0 = hipSetDevice(e->device);
     if (st0 == hipSuccess) st0 = hipStreamSynchronize(e->stream);
@@ -443,7 +476,14 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     int r;
     if ((r = up((void**)&blk.d_tasks, tasks.data(), tasks.size() * sizeof(Task)))) return r;
     if ((r = up((void**)&blk.d_reduce, reduce.data(), reduce.size() * sizeof(Task)))) return r;
-    if (!tasks.empty()) HIP_TRY(hipMalloc((void**)&blk.d_task_se, tasks.size() * sizeof(double)));
+    for (int c = 0; c < 2; ++c) {
+        if ((r = up((void**)&blk.d_dual[c], dual[c].data(), dual[c].size() * sizeof(Task)))) return r;
+        blk.n_dual[c] = (int32_t)dual[c].size();
+        blk.h_dual[c] = std::move(dual[c]);
+    }
+    if ((r = up((void**)&blk.d_sq_tasks, sq_all.data(), sq_all.size() * sizeof(Task)))) return r;
+    blk.n_sq = (int32_t)sq_all.size();
+    if (!sq_all.empty()) HIP_TRY(hipMalloc((void**)&blk.d_task_se, sq_all.size() * sizeof(double)));
     blk.h_tasks = std::move(tasks);
     blk.h_reduce = std::move(reduce);
     // Partial workspace sized for the larger side.
@@ -649,8 +689,13 @@ int als_read_factors(als_engine* e, int side, int64_t row0, int64_t n_rows, void
 namespace {
 
 // One half (or one chunk of it): the FULL + PARTIAL launch, then the REDUCE launch.
+struct DualLaunch {
+    const Task* t[2] = {nullptr, nullptr};
+    int32_t n[2] = {0, 0};
+};
+
 int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_t n_tasks, const Task* reduce,
-                int32_t n_reduce, bool first_chunk) {
+                int32_t n_reduce, bool first_chunk, const DualLaunch& dl) {
     Block& b = e->blk[side];
     const Factors& self = e->fac[side];
     const Factors& opp = e->fac[1 - side];
@@ -699,6 +744,13 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
         a.opp_split = e->d_split;
     }
     HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves, b.presplit, false));
+    for (int c = 0; c < 2; ++c)
+        if (dl.n[c] > 0) {
+            cfk::SolveArgs d = a;
+            d.tasks = dl.t[c];
+            d.n_tasks = dl.n[c];
+            HIP_TRY(cfk::launch_dual(e->kp, c == 0 ? 2 : 4, d, e->stream));
+        }
     if (e->timing) HIP_TRY(hipEventRecord(rec.ev[1], e->stream));
     if (n_reduce > 0) {
         a.tasks = reduce;
@@ -720,7 +772,12 @@ int als_solve_half(als_engine* e, int side, float lambda) {
     if (int r = check_side(side)) return r;
     Block& b = e->blk[side];
     if (!b.set) return fail(ALS_ERR_STATE, "als_solve_half: no block set for side %d", side);
-    return launch_half(e, side, lambda, b.d_tasks, b.n_tasks, b.d_reduce, b.n_reduce, true);
+    DualLaunch dl;
+    for (int c = 0; c < 2; ++c) {
+        dl.t[c] = b.d_dual[c];
+        dl.n[c] = b.n_dual[c];
+    }
+    return launch_half(e, side, lambda, b.d_tasks, b.n_tasks, b.d_reduce, b.n_reduce, true, dl);
 }
 
 int als_set_chunks(als_engine* e, int side, int n_chunks, const int64_t* row_bounds) {
@@ -747,9 +804,10 @@ int als_set_chunks(als_engine* e, int side, int n_chunks, const int64_t* row_bou
             off[c + 1] = (int32_t)out.size();
         }
     };
-    std::vector<Task> ct, cr;
+    std::vector<Task> ct, cr, cdl[2];
     split(b.h_tasks, ct, b.coff);
     split(b.h_reduce, cr, b.croff);
+    for (int c = 0; c < 2; ++c) split(b.h_dual[c], cdl[c], b.cdoff[c]);
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
     (void)hipFree(b.d_ctasks);
@@ -763,6 +821,14 @@ int als_set_chunks(als_engine* e, int side, int n_chunks, const int64_t* row_bou
         HIP_TRY(hipMalloc((void**)&b.d_creduce, cr.size() * sizeof(Task)));
         HIP_TRY(hipMemcpy(b.d_creduce, cr.data(), cr.size() * sizeof(Task), hipMemcpyHostToDevice));
     }
+    for (int c = 0; c < 2; ++c) {
+        (void)hipFree(b.d_cdual[c]);
+        b.d_cdual[c] = nullptr;
+        if (!cdl[c].empty()) {
+            HIP_TRY(hipMalloc((void**)&b.d_cdual[c], cdl[c].size() * sizeof(Task)));
+            HIP_TRY(hipMemcpy(b.d_cdual[c], cdl[c].data(), cdl[c].size() * sizeof(Task), hipMemcpyHostToDevice));
+        }
+    }
     return ALS_OK;
 }
 
@@ -773,8 +839,13 @@ int als_solve_half_chunk(als_engine* e, int side, float lambda, int chunk) {
     if (!b.set || b.coff.empty()) return fail(ALS_ERR_STATE, "als_solve_half_chunk: no chunks set for side %d", side);
     if (chunk < 0 || chunk + 1 >= (int)b.coff.size())
         return fail(ALS_ERR_INVALID_ARGUMENT, "chunk %d out of range (%d chunks)", chunk, (int)b.coff.size() - 1);
+    DualLaunch dl;
+    for (int c = 0; c < 2; ++c) {
+        dl.t[c] = b.d_cdual[c] + b.cdoff[c][chunk];
+        dl.n[c] = b.cdoff[c][chunk + 1] - b.cdoff[c][chunk];
+    }
     return launch_half(e, side, lambda, b.d_ctasks + b.coff[chunk], b.coff[chunk + 1] - b.coff[chunk],
-                       b.d_creduce + b.croff[chunk], b.croff[chunk + 1] - b.croff[chunk], chunk == 0);
+                       b.d_creduce + b.croff[chunk], b.croff[chunk + 1] - b.croff[chunk], chunk == 0, dl);
 }
 
 int als_predict(als_engine* e, const int64_t* user_rows, int64_t n_users, const int64_t* movie_rows,
@@ -830,8 +901,8 @@ int als_sq_error(als_engine* e, int side, double* sum_sq_error, int64_t* count) 
     HIP_TRY(hipSetDevice(e->device));
     if (int r = wait_gathers(e, true, true)) return r;
     cfk::SqErrArgs a{};
-    a.tasks = b.d_tasks;
-    a.n_tasks = b.n_tasks;
+    a.tasks = b.d_sq_tasks;
+    a.n_tasks = b.n_sq;
     a.col = b.d_col;
     a.rat = b.d_rat;
     a.opp = opp.ptr;
@@ -840,8 +911,8 @@ int als_sq_error(als_engine* e, int side, double* sum_sq_error, int64_t* count) 
     a.task_se = b.d_task_se;
     a.sentinel = (int32_t)b.n_opp_rows;
     HIP_TRY(cfk::launch_sq_error(e->precision, e->kp, a, e->stream));
-    std::vector<double> se(b.n_tasks);
-    if (b.n_tasks > 0)
+    std::vector<double> se(b.n_sq);
+    if (b.n_sq > 0)
         HIP_TRY(hipMemcpyAsync(se.data(), b.d_task_se, se.size() * sizeof(double), hipMemcpyDeviceToHost, e->stream));
     if (int r = sync_checked(e)) return r;
     double s = 0.0;
@@ -1033,13 +1104,14 @@ int als_comm_wait(als_engine* e) {
     return wait_gathers(e, true, true);
 }
 
-int als_block_path(const als_engine* e, int side, int* gram_path, int* presplit, int64_t* chunk) {
+int als_block_path(const als_engine* e, int side, int* gram_path, int* presplit, int64_t* chunk, int64_t* n_dual_rows) {
     if (int r = check_engine(e)) return r;
     if (int r = check_side(side)) return r;
     const Block& b = e->blk[side];
     if (gram_path) *gram_path = (int)e->path;
     if (presplit) *presplit = b.presplit ? 1 : 0;
     if (chunk) *chunk = b.set ? chunk_entries(b.nnz_padded) : 0;
+    if (n_dual_rows) *n_dual_rows = b.n_dual[0] + b.n_dual[1];
     return ALS_OK;
 }
 
@@ -1047,7 +1119,7 @@ int als_block_stats(const als_engine* e, int side, int64_t* n_tasks, int64_t* n_
     if (int r = check_engine(e)) return r;
     if (int r = check_side(side)) return r;
     const Block& b = e->blk[side];
-    if (n_tasks) *n_tasks = b.n_tasks;
+    if (n_tasks) *n_tasks = b.n_tasks + b.n_dual[0] + b.n_dual[1];
     if (n_reduce) *n_reduce = b.n_reduce;
     if (nnz_padded) *nnz_padded = b.nnz_padded;
     return ALS_OK;

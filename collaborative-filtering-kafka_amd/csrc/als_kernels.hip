@@ -574,14 +574,42 @@ constexpr bool tiles_in_lds() { return C > 4; }
 template <int C>
 constexpr int tile_lds_floats() { return tiles_in_lds<C>() ? MfmaAcc<C>::NT * 4 * 64 : 0; }
 
+// Logical in-block entry index of physical position q of a row's padded range (inverse of block_position).
+__device__ __forceinline__ int logical_entry(int q) {
+    const int w = q % BLOCK_ENTRIES;
+    return q - w + (w % BLOCK_SUBSTEPS) * 4 + w / BLOCK_SUBSTEPS;
+}
+
 // T: working tiles (RegTiles / LdsTiles), A0: kept copy of the scaled system (RegStore / LdsTiles).
-template <int C, class TT, class KT>
+// DUAL: the system is the entry Gram of a short row (als_solve_dual): unknown 16b + j = the row's entry at
+// physical position 16b + j, real when that entry exists (padding entries get an identity row), and the
+// solution alpha goes to buf[16b + j] (read by the caller after a wave_sync) instead of a factor row.
+template <int C, bool DUAL = false, class TT, class KT>
 __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc)[C], float* buf, const Task& tk,
                                             const SolveArgs& a, int lane) {
     const int g = lane >> 4, j = lane & 15;
     float* out = (float*)a.out + (a.row_offset + tk.row) * (int64_t)(16 * C);
+    auto is_real = [&](int b) { return DUAL ? logical_entry(16 * b + j) < tk.nent : C * j + b < a.k; };
+    auto emit = [&](const float (&xs)[C]) {   // xs = solution in the scaled variables, times scol
+        if constexpr (DUAL) {
+            wave_sync();
+            if (g == 0) {
+#pragma unroll
+                for (int b = 0; b < C; ++b) buf[16 * b + j] = is_real(b) ? xs[b] : 0.f;
+            }
+        } else if (g == 0) {
+            using VT = typename VecC<C>::type;
+            VT o;
+#pragma unroll
+            for (int b = 0; b < C; ++b) o[b] = is_real(b) ? xs[b] : 0.f;
+            *(VT*)(out + C * j) = o;
+        }
+    };
     if (tk.ndeg == 0) {   // cannot occur in the reference (entities exist only once rated); defined as 0
-        if (g == 0) {
+        if (DUAL) {
+            float z[C] = {};
+            emit(z);
+        } else if (g == 0) {
 #pragma unroll
             for (int b = 0; b < C; ++b) out[C * j + b] = 0.f;
         }
@@ -599,7 +627,7 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 #pragma unroll
     for (int b = 0; b < C; ++b) {
         f32x4 t = T.get(tile_index<C>(b, b));
-        const bool real = C * j + b < a.k;
+        const bool real = is_real(b);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const bool diag = diag_lane && jr == r;
@@ -721,13 +749,10 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
     float x[C];
     solve_vec(b0, x);
     if (a.flags & SOLVE_FLAG_SKIP_REFINE) {   // diagnostics only
-        if (g == 0) {
-            using VT = typename VecC<C>::type;
-            VT o;
+        float xs[C];
 #pragma unroll
-            for (int b = 0; b < C; ++b) o[b] = (C * j + b < a.k) ? x[b] * scol[b] : 0.f;
-            *(VT*)(out + C * j) = o;
-        }
+        for (int b = 0; b < C; ++b) xs[b] = x[b] * scol[b];
+        emit(xs);
         return;
     }
 
@@ -777,13 +802,10 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
     for (int b = 0; b < C; ++b) r[b] = b0[b] - buf[16 * b + j] - (C > 1 ? col_sum(res[b]) : 0.f);
     float dx[C];
     solve_vec(r, dx);
-    if (g == 0) {
-        using VT = typename VecC<C>::type;
-        VT o;
+    float xs[C];
 #pragma unroll
-        for (int b = 0; b < C; ++b) o[b] = (C * j + b < a.k) ? (x[b] + dx[b]) * scol[b] : 0.f;
-        *(VT*)(out + C * j) = o;
-    }
+    for (int b = 0; b < C; ++b) xs[b] = (x[b] + dx[b]) * scol[b];
+    emit(xs);
 }
 
 // Waves (tasks) per workgroup of the MFMA kernel: 4, or 2 at KP = 128, whose 72 KB of per-wave LDS tiles
@@ -1283,6 +1305,113 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Short rows in entry space (fp32, split-bf16 MFMA)
+// ---------------------------------------------------------------------------------------------------
+// For a row with n <= 16 * CD entries (its 1 or 2 padded 32-entry blocks, CD = 2 or 4) the update
+//   m = (Y^T Y + lambda n I_k)^{-1} Y^T r      (MFeatureCalculator.java:85-99, Y = the n x k gathered rows)
+// equals  m = Y^T alpha  with  (Y Y^T + lambda n I_n) alpha = r  (push-through identity; the same nonzero
+// spectrum and conditioning), an n x n system instead of k x k: at k = 128 a 64-entry user costs a 64 x 64
+// solve instead of 128 x 128. The entry Gram Y Y^T needs no operand transposition: lane (g, i) loads the 32-B
+// piece [32s + 8g, 32s + 8g + 8) of entry 16I + i's factor row, which is directly the A (and B) operand
+// "row i, k = 8g..8g+7" of v_mfma_f32_16x16x32_bf16 for feature chunk s, split exactly into h/m/l bf16 terms
+// as on the primal path. Entries are in physical (padded, block-interleaved) order; padding entries gather
+// the zero sentinel row with rating 0 and get an identity row (solve_tiles<DUAL>), so alpha is 0 there.
+template <int KP, int CD>
+__global__ __launch_bounds__(64 * WAVES, 2) void als_solve_dual(SolveArgs a) {
+    constexpr int NS = KP / 32;      // 32-feature chunks = MFMA K steps
+    constexpr int NF = KP / 64;      // output features per lane
+    using Acc = MfmaAcc<CD>;
+    __shared__ __attribute__((aligned(16))) float sbuf[WAVES][16 * CD];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tid = blockIdx.x * WAVES + wave;
+    if (tid >= a.n_tasks) return;   // wave-uniform; no workgroup barriers below
+    const Task tk = load_task(a.tasks + tid);
+    float* buf = sbuf[wave];
+    const int g = lane >> 4, i = lane & 15;
+    const float* opp = (const float*)a.opp;
+    int cidx[CD];
+    float rr[CD];
+#pragma unroll
+    for (int I = 0; I < CD; ++I) {
+        cidx[I] = a.col[tk.begin + 16 * I + i];
+        rr[I] = a.rat[tk.begin + 16 * I + i];
+    }
+    f32x4 acc[Acc::NT];
+#pragma unroll
+    for (int p = 0; p < Acc::NT; ++p) acc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* obase = (const char*)(opp + 8 * g);
+    auto load = [&](int s, f32x8 (&y)[CD]) {
+#pragma unroll
+        for (int I = 0; I < CD; ++I)
+            y[I] = *(const f32x8*)(obase + (uint32_t)cidx[I] * (uint32_t)(KP * sizeof(float)) + s * 128);
+    };
+    f32x8 yc[CD], yn[CD];
+    load(0, yc);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        if (s + 1 < NS) load(s + 1, yn);
+        u32x4 H[CD], M[CD], L[CD];
+#pragma unroll
+        for (int I = 0; I < CD; ++I)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                unsigned h, m, l;
+                split3(yc[I][2 * q], yc[I][2 * q + 1], h, m, l);
+                pin(h);
+                pin(m);
+                pin(l);
+                H[I][q] = h;
+                M[I][q] = m;
+                L[I][q] = l;
+            }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int I = 0; I < CD; ++I)
+#pragma unroll
+            for (int J = I; J < CD; ++J) {
+                f32x4 t = acc[tile_index<CD>(I, J)];
+                t = mfma_k32(M[I], M[J], t);
+                t = mfma_k32(H[I], L[J], t);
+                t = mfma_k32(L[I], H[J], t);
+                t = mfma_k32(H[I], M[J], t);
+                t = mfma_k32(M[I], H[J], t);
+                t = mfma_k32(H[I], H[J], t);
+                acc[tile_index<CD>(I, J)] = t;
+            }
+        MFMA_DRAIN();
+        if (s + 1 < NS) {
+#pragma unroll
+            for (int I = 0; I < CD; ++I) yc[I] = yn[I];
+        }
+    }
+    // right-hand side r in the per-lane partial layout of solve_tiles (element j of block b on row g = 0)
+    float rhs[CD];
+#pragma unroll
+    for (int b = 0; b < CD; ++b) rhs[b] = g == 0 ? rr[b] : 0.f;
+    RegTiles<CD> T{acc};
+    RegStore<CD> A0;
+    solve_tiles<CD, true>(T, A0, rhs, buf, tk, a, lane);
+    wave_sync();
+    // m = Y^T alpha: lane l owns features l + 64 f; entries with alpha = 0 (padding, or exactly 0) are skipped
+    float xo[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) xo[f] = 0.f;
+#pragma unroll
+    for (int I = 0; I < CD; ++I)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const float al = buf[16 * I + e];
+            const int c = __builtin_amdgcn_readlane(cidx[I], e);
+            const float* row = opp + (int64_t)c * KP + lane;
+#pragma unroll
+            for (int f = 0; f < NF; ++f) xo[f] += row[64 * f] * al;
+        }
+    float* out = (float*)a.out + (a.row_offset + tk.row) * (int64_t)KP + lane;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) out[64 * f] = (lane + 64 * f < a.k) ? xo[f] : 0.f;
+}
+
+// ---------------------------------------------------------------------------------------------------
 // VALU Gram path (LDS-staged rows), fp32 and fp64
 // ---------------------------------------------------------------------------------------------------
 template <class T, int KP>
@@ -1554,6 +1683,16 @@ hipError_t launch_presplit(const float* src, void* dst, int64_t n_rows, hipStrea
     const int64_t pieces = n_rows * 16;
     if (pieces <= 0) return hipSuccess;
     als_presplit<<<(unsigned)((pieces + 255) / 256), 256, 0, s>>>(src, (unsigned*)dst, pieces);
+    return hipGetLastError();
+}
+
+hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s) {
+    if (a.n_tasks <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)blocks_for(a.n_tasks);
+    if (kp == 64 && cd == 2) als_solve_dual<64, 2><<<grid, 64 * WAVES, 0, s>>>(a);
+    else if (kp == 128 && cd == 2) als_solve_dual<128, 2><<<grid, 64 * WAVES, 0, s>>>(a);
+    else if (kp == 128 && cd == 4) als_solve_dual<128, 4><<<grid, 64 * WAVES, 0, s>>>(a);
+    else return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -124,7 +124,8 @@ def test_presplit_path_with_bf16_exact_extreme_ratings(cfk, oracle_mod):
     ref = oracle_mod.update_side(b.user, F, LAM, "f64")
     ref32 = oracle_mod.update_side(b.user, F.astype(np.float32), LAM, "f32")
     eng = _engine(cfk, 64, "f32", 1, ds.shard_block(1), len(b.movie.ids), F.astype(np.float32))
-    assert eng.block_path(1) == {"gram_path": "mfma_split", "presplit": True, "chunk": eng.block_path(1)["chunk"]}
+    bp = eng.block_path(1)
+    assert bp["gram_path"] == "mfma_split" and bp["presplit"]
     eng.solve_half(1, LAM)
     got = eng.read_factors(1)
     eng.close()

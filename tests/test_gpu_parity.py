@@ -487,3 +487,34 @@ def test_comm_init_group_one_engine(cfk):
     with pytest.raises(ALSError, match="ALS_ERR_STATE"):
         cfk.ALSEngine.comm_init_group([e])            # already has a communicator
     e.close()
+
+
+@pytest.mark.parametrize("k", [64, 128])
+def test_short_rows_entry_space_matches_kxk(cfk, oracle_mod, monkeypatch, k):
+    """Short rows (1 padded block at k = 64, <= 2 at k = 128) are solved in entry space by als_solve_dual,
+    (Y Y^T + lambda n I) alpha = r, m = Y^T alpha: the same solution as the k x k system. Against the fp64
+    oracle at the every-k bar, and against the k x k path (ALS_DUAL=0) to fp32 accuracy."""
+    ds, b = _synthetic(cfk, oracle_mod)                     # users of ~30 ratings: most rows are short
+    F = np.random.default_rng(k + 7).random((len(b.movie.ids), k))
+    blk = ds.shard_block(1)
+    outs = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("ALS_DUAL", env)
+        eng = cfk.ALSEngine(k, "f32")
+        eng.alloc_factors(0, len(b.movie.ids))
+        eng.alloc_factors(1, blk["n_rows"])
+        eng.set_block(1, blk["row_ptr"], blk["col"], blk["ratings"], 0, len(b.movie.ids))
+        dual = eng.block_path(1)["dual_rows"]
+        assert (dual > blk["n_rows"] // 3) if env == "1" else dual == 0
+        eng.write_factors(0, F.astype(np.float32))
+        eng.solve_half(1, LAM)
+        outs.append(eng.read_factors(1))
+        eng.close()
+    ref = oracle_mod.update_side(b.user, F, LAM, "f64")
+    ref32 = oracle_mod.update_side(b.user, F.astype(np.float32), LAM, "f32")
+    norm = np.linalg.norm(ref, axis=1)
+    for got in outs:
+        rel = np.linalg.norm(got - ref, axis=1) / norm
+        rel_ref = np.linalg.norm(ref32 - ref, axis=1) / norm
+        assert np.percentile(rel, 99) <= max(2 * np.percentile(rel_ref, 99), 2e-5)
+        assert rel.max() <= max(3 * rel_ref.max(), 1e-4), (rel.max(), rel_ref.max())

@@ -35,6 +35,8 @@ def is_reduce(name):
 def role_of(name, grid, grids):
     if "als_solve" not in name:
         return None
+    if "als_solve_dual" in name:
+        return "dual"
     if is_reduce(name):
         return "reduce"
     big = sorted(grids, reverse=True)
@@ -63,7 +65,7 @@ def main(tag, name):
     if st:
         shutil.copy(st[0], os.path.join(dst, "kernel_stats.csv"))
     grid = lambda r: int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)
-    grids = {grid(r) for r in tr if "als_solve" in r["Kernel_Name"] and not is_reduce(r["Kernel_Name"])}
+    grids = {grid(r) for r in tr if "als_solve_mfma" in r["Kernel_Name"] and not is_reduce(r["Kernel_Name"])}
     dur = defaultdict(list)
     for r in tr:
         role = role_of(r["Kernel_Name"], grid(r), grids)
@@ -75,7 +77,7 @@ def main(tag, name):
     # --- PMC passes ---
     def per_role(pattern):
         rows = load_rows(pattern)
-        g = {int(r["Grid_Size"]) for r in rows if "als_solve" in r["Kernel_Name"] and not is_reduce(r["Kernel_Name"])}
+        g = {int(r["Grid_Size"]) for r in rows if "als_solve_mfma" in r["Kernel_Name"] and not is_reduce(r["Kernel_Name"])}
         acc = defaultdict(lambda: defaultdict(list))
         disp = defaultdict(lambda: defaultdict(float))
         for r in rows:
@@ -89,7 +91,7 @@ def main(tag, name):
     fetch = per_role(f"{src}/fetch/**/*counter_collection.csv")
     write = per_role(f"{src}/write/**/*counter_collection.csv")
     traffic = {}
-    for role in ("movie", "user", "reduce"):
+    for role in ("movie", "user", "reduce", "dual"):
         if role in fetch and role in write:
             traffic[role] = {"fetch_bytes_x2": fetch[role]["FETCH_SIZE"] * 1024 * 2,
                              "write_bytes": write[role]["WRITE_SIZE"] * 1024}
