@@ -55,11 +55,11 @@ struct Block {
     Task* d_creduce = nullptr;      // chunk-major REDUCE tasks
     std::vector<int32_t> coff, croff;   // chunk c = d_ctasks[coff[c], coff[c+1]), d_creduce[croff[c], ...)
     // short rows solved in entry space (cfk::launch_dual), by entry-tile count cd = 2 (1 block) / 4 (2 blocks)
-    Task* d_dual[2] = {nullptr, nullptr};
-    int32_t n_dual[2] = {0, 0};
-    std::vector<Task> h_dual[2];
-    Task* d_cdual[2] = {nullptr, nullptr};
-    std::vector<int32_t> cdoff[2];
+    Task* d_dual[3] = {nullptr, nullptr, nullptr};
+    int32_t n_dual[3] = {0, 0, 0};
+    std::vector<Task> h_dual[3];
+    Task* d_cdual[3] = {nullptr, nullptr, nullptr};
+    std::vector<int32_t> cdoff[3];
     Task* d_sq_tasks = nullptr;     // every FULL + PARTIAL task incl. the short rows (als_sq_error)
     int32_t n_sq = 0;
     bool presplit = false;          // gather a pre-split (bf16 h/m/l) copy of the opposite table
@@ -103,6 +103,10 @@ struct als_engine {
     int32_t debug_flags = 0;        // ALS_DEBUG_SKIP_SOLVE=1 -> cfk::SOLVE_FLAG_SKIP_SOLVE (tools/kbench.py only)
     uint32_t debug_gen_skew = 0;    // ALS_DEBUG_REDUCE_GEN_SKEW=n: REDUCE decodes with generation + n (tests the
                                     // integrity check: every slot then reads as written by another launch)
+    // ALS_REFINE_MIN_PIVOT (cfk::SolveArgs): 0.45 keeps the worst per-row error ratio to the reference's own fp32
+    // path where always refining puts it (0.41, tools/refine_accuracy.py; 0.30 lets it reach 1.2), and skips the
+    // step for nearly every Netflix-shape row (k = 128 user half 17.7 -> 14.9 ms); > 1 always refines
+    float refine_min_pivot = 0.45f;
     bool debug_fixed_gen = false;   // ALS_DEBUG_FIXED_GEN=1: every launch uses generation 1, so partial slots of
                                     // repeated launches are bitwise comparable (als_debug_copy_partials)
     ncclComm_t comm = nullptr;      // RCCL communicator over the G engines (one per GPU) of a sharded run
@@ -164,7 +168,7 @@ void free_block(Block& b) {
     (void)hipFree(b.d_task_se);
     (void)hipFree(b.d_ctasks);
     (void)hipFree(b.d_creduce);
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < 3; ++c) {
         (void)hipFree(b.d_dual[c]);
         (void)hipFree(b.d_cdual[c]);
     }
@@ -239,6 +243,7 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
         if (env[0] == '1') e->debug_flags |= cfk::SOLVE_FLAG_SKIP_SOLVE;
     if (const char* env = getenv("ALS_DEBUG_REDUCE_GEN_SKEW")) e->debug_gen_skew = (uint32_t)atoi(env);
     if (const char* env = getenv("ALS_DEBUG_FIXED_GEN")) e->debug_fixed_gen = env[0] == '1';
+    if (const char* env = getenv("ALS_REFINE_MIN_PIVOT")) e->refine_min_pivot = (float)atof(env);
     if (const char* env = getenv("ALS_DEBUG_SKIP_REFINE"))
         if (env[0] == '1') e->debug_flags |= cfk::SOLVE_FLAG_SKIP_REFINE;
     hipError_t st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
@@ -395,19 +400,20 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
             reduce.push_back(r);
         }
     }
-    // Short rows in entry space (split-bf16 path): rows of <= 2 blocks at KP = 128, 1 block at KP = 64 solve the
+    // Short rows in entry space (split-bf16 path): rows of <= 3 blocks at KP = 128, 1 block at KP = 64 solve the
     // (padded entries)^2 system of als_solve_dual instead of the KP x KP one. ALS_DUAL=0 turns it off.
     std::vector<Task> sq_all = tasks;
-    std::vector<Task> dual[2];
+    std::vector<Task> dual[3];
     {
-        const int max_cd = e->path != Path::MFMA_SPLIT ? 0 : e->kp == 128 ? 4 : e->kp == 64 ? 2 : 0;
+        int max_cd = e->path != Path::MFMA_SPLIT ? 0 : e->kp == 128 ? 6 : e->kp == 64 ? 2 : 0;
+        if (const char* env = getenv("ALS_DUAL_MAX_CD")) max_cd = std::min(max_cd, atoi(env));
         bool on = max_cd > 0;
         if (const char* env = getenv("ALS_DUAL")) on = on && env[0] != '0';
         if (on) {
             std::vector<Task> keep;
             for (const Task& t : tasks) {
                 const int cd = 2 * ((t.nent + cfk::BLOCK_ENTRIES - 1) / cfk::BLOCK_ENTRIES);
-                if (t.kind == cfk::TASK_FULL && t.ndeg > 0 && cd <= max_cd) dual[cd == 2 ? 0 : 1].push_back(t);
+                if (t.kind == cfk::TASK_FULL && t.ndeg > 0 && cd <= max_cd) dual[cd / 2 - 1].push_back(t);
                 else keep.push_back(t);
             }
             tasks.swap(keep);
@@ -476,7 +482,7 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     int r;
     if ((r = up((void**)&blk.d_tasks, tasks.data(), tasks.size() * sizeof(Task)))) return r;
     if ((r = up((void**)&blk.d_reduce, reduce.data(), reduce.size() * sizeof(Task)))) return r;
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < 3; ++c) {
         if ((r = up((void**)&blk.d_dual[c], dual[c].data(), dual[c].size() * sizeof(Task)))) return r;
         blk.n_dual[c] = (int32_t)dual[c].size();
         blk.h_dual[c] = std::move(dual[c]);
@@ -690,8 +696,8 @@ namespace {
 
 // One half (or one chunk of it): the FULL + PARTIAL launch, then the REDUCE launch.
 struct DualLaunch {
-    const Task* t[2] = {nullptr, nullptr};
-    int32_t n[2] = {0, 0};
+    const Task* t[3] = {nullptr, nullptr, nullptr};
+    int32_t n[3] = {0, 0, 0};
 };
 
 int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_t n_tasks, const Task* reduce,
@@ -727,6 +733,7 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
     if (++e->gen == 0) e->gen = 1;
     a.gen = e->debug_fixed_gen ? 1u : e->gen;
     a.integrity = e->d_integrity;
+    a.refine_min_pivot = e->refine_min_pivot;
     TimingRec rec{side, {nullptr, nullptr, nullptr}};
     if (e->timing) {
         for (auto& ev : rec.ev) {
@@ -744,12 +751,12 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
         a.opp_split = e->d_split;
     }
     HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves, b.presplit, false));
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c < 3; ++c)
         if (dl.n[c] > 0) {
             cfk::SolveArgs d = a;
             d.tasks = dl.t[c];
             d.n_tasks = dl.n[c];
-            HIP_TRY(cfk::launch_dual(e->kp, c == 0 ? 2 : 4, d, e->stream));
+            HIP_TRY(cfk::launch_dual(e->kp, 2 * (c + 1), d, e->stream));
         }
     if (e->timing) HIP_TRY(hipEventRecord(rec.ev[1], e->stream));
     if (n_reduce > 0) {
@@ -773,7 +780,7 @@ int als_solve_half(als_engine* e, int side, float lambda) {
     Block& b = e->blk[side];
     if (!b.set) return fail(ALS_ERR_STATE, "als_solve_half: no block set for side %d", side);
     DualLaunch dl;
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < 3; ++c) {
         dl.t[c] = b.d_dual[c];
         dl.n[c] = b.n_dual[c];
     }
@@ -804,10 +811,10 @@ int als_set_chunks(als_engine* e, int side, int n_chunks, const int64_t* row_bou
             off[c + 1] = (int32_t)out.size();
         }
     };
-    std::vector<Task> ct, cr, cdl[2];
+    std::vector<Task> ct, cr, cdl[3];
     split(b.h_tasks, ct, b.coff);
     split(b.h_reduce, cr, b.croff);
-    for (int c = 0; c < 2; ++c) split(b.h_dual[c], cdl[c], b.cdoff[c]);
+    for (int c = 0; c < 3; ++c) split(b.h_dual[c], cdl[c], b.cdoff[c]);
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->stream));
     (void)hipFree(b.d_ctasks);
@@ -821,7 +828,7 @@ int als_set_chunks(als_engine* e, int side, int n_chunks, const int64_t* row_bou
         HIP_TRY(hipMalloc((void**)&b.d_creduce, cr.size() * sizeof(Task)));
         HIP_TRY(hipMemcpy(b.d_creduce, cr.data(), cr.size() * sizeof(Task), hipMemcpyHostToDevice));
     }
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < 3; ++c) {
         (void)hipFree(b.d_cdual[c]);
         b.d_cdual[c] = nullptr;
         if (!cdl[c].empty()) {
@@ -840,7 +847,7 @@ int als_solve_half_chunk(als_engine* e, int side, float lambda, int chunk) {
     if (chunk < 0 || chunk + 1 >= (int)b.coff.size())
         return fail(ALS_ERR_INVALID_ARGUMENT, "chunk %d out of range (%d chunks)", chunk, (int)b.coff.size() - 1);
     DualLaunch dl;
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < 3; ++c) {
         dl.t[c] = b.d_cdual[c] + b.cdoff[c][chunk];
         dl.n[c] = b.cdoff[c][chunk + 1] - b.cdoff[c][chunk];
     }
@@ -1111,7 +1118,7 @@ int als_block_path(const als_engine* e, int side, int* gram_path, int* presplit,
     if (gram_path) *gram_path = (int)e->path;
     if (presplit) *presplit = b.presplit ? 1 : 0;
     if (chunk) *chunk = b.set ? chunk_entries(b.nnz_padded) : 0;
-    if (n_dual_rows) *n_dual_rows = b.n_dual[0] + b.n_dual[1];
+    if (n_dual_rows) *n_dual_rows = b.n_dual[0] + b.n_dual[1] + b.n_dual[2];
     return ALS_OK;
 }
 
@@ -1119,7 +1126,7 @@ int als_block_stats(const als_engine* e, int side, int64_t* n_tasks, int64_t* n_
     if (int r = check_engine(e)) return r;
     if (int r = check_side(side)) return r;
     const Block& b = e->blk[side];
-    if (n_tasks) *n_tasks = b.n_tasks + b.n_dual[0] + b.n_dual[1];
+    if (n_tasks) *n_tasks = b.n_tasks + b.n_dual[0] + b.n_dual[1] + b.n_dual[2];
     if (n_reduce) *n_reduce = b.n_reduce;
     if (nnz_padded) *nnz_padded = b.nnz_padded;
     return ALS_OK;

@@ -58,6 +58,7 @@ struct SolveArgs {
     const void* opp_split;  // MFMA_SPLIT + presplit: the opposite table as bf16 h/m/l pieces (als_presplit)
     uint32_t gen;           // launch generation (PARTIAL and its REDUCE share it): keys the partial-slot encoding
     uint32_t* integrity;    // device record of partial slots that failed their check (see als_kernels.hip)
+    float refine_min_pivot; // MFMA tile solve: skip the refinement step when every scaled pivot >= this (> 1: never)
 };
 // Partial-slot integrity record (device, 4 words): [0] REDUCE tasks that found a bad slot, [1] generation, [2] slot,
 // [3] row of the first failure. Read back by every synchronising call of the engine.

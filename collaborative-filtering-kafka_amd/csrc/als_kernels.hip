@@ -500,11 +500,12 @@ __device__ __forceinline__ float row_sum_to_last(float v) {
 // which the caller guarantees by Jacobi-scaling the system to a unit diagonal (every later pivot is a
 // Schur-complement diagonal of a unit-diagonal SPD matrix, so it stays in (0, 1]).
 template <bool SWAP>
-__device__ __forceinline__ void sweep_tile(f32x4& a, int lane) {
+__device__ __forceinline__ void sweep_tile(f32x4& a, int lane, float& nrd_min) {
     static_for<0, 16>([&](auto P_) {
         constexpr int p = decltype(P_)::value;
         constexpr int pg = p >> 2, pr = p & 3;
         const float nrd = __builtin_amdgcn_rcpf(-bcast(a[pr], 16 * pg + p));   // -1 / d
+        nrd_min = fminf(nrd_min, nrd);                                          // -1 / (smallest pivot)
         const bool piv = lane == 16 * pg + p;   // 16 lane masks, CSE-d across the 4 diagonal tiles (SGPRs)
         a[pr] = piv ? a[pr] - 1.f : a[pr];
         const float t = (SWAP ? col_bcast_swap<pg>(a[pr]) : col_bcast<pg>(a[pr])) * nrd;   // a[p][c] (d - 1 at c = p) * (-1/d)
@@ -661,10 +662,11 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
     for (int b = 0; b < C; ++b) b0[b] = col_sum(rhs_acc[b]) * scol[b];
 
     // ---- factorisation (matrix part only) ----
+    float nrd_min = -1.f;
     static_for<0, C>([&](auto P_) {
         constexpr int P = decltype(P_)::value;
         f32x4 S = T.get(tile_index<C>(P, P));
-        sweep_tile<(16 * C >= CFK_COL_SWAP)>(S, lane);
+        sweep_tile<(16 * C >= CFK_COL_SWAP)>(S, lane, nrd_min);
         T.put(tile_index<C>(P, P), S);
         // Block columns J in DESCENDING order: V'_PJ only updates T_IJ (P < I <= J) from the still-unreplaced
         // T_PI (I <= J), so block row P can take V'_PJ right away and one V is live at a time. Every T_IJ
@@ -748,6 +750,16 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
     };
     float x[C];
     solve_vec(b0, x);
+    // Well-conditioned systems skip the refinement step: every pivot of the scaled (unit-diagonal) system is a
+    // Schur-complement diagonal in (0, 1]; when the smallest is >= a.refine_min_pivot the block factorisation's
+    // error is already below the reference's own fp32 LU error. The test is wave-uniform.
+    if (-1.f / nrd_min >= a.refine_min_pivot) {
+        float xs[C];
+#pragma unroll
+        for (int b = 0; b < C; ++b) xs[b] = x[b] * scol[b];
+        emit(xs);
+        return;
+    }
     if (a.flags & SOLVE_FLAG_SKIP_REFINE) {   // diagnostics only
         float xs[C];
 #pragma unroll
@@ -1317,11 +1329,13 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
 // as on the primal path. Entries are in physical (padded, block-interleaved) order; padding entries gather
 // the zero sentinel row with rating 0 and get an identity row (solve_tiles<DUAL>), so alpha is 0 there.
 template <int KP, int CD>
-__global__ __launch_bounds__(64 * WAVES, 2) void als_solve_dual(SolveArgs a) {
+__global__ __launch_bounds__(64 * WAVES, CD <= 4 ? 2 : 1) void als_solve_dual(SolveArgs a) {
     constexpr int NS = KP / 32;      // 32-feature chunks = MFMA K steps
     constexpr int NF = KP / 64;      // output features per lane
     using Acc = MfmaAcc<CD>;
     __shared__ __attribute__((aligned(16))) float sbuf[WAVES][16 * CD];
+    constexpr int TL = tile_lds_floats<CD>();
+    __shared__ __attribute__((aligned(16))) float tiles_lds[WAVES][TL > 0 ? TL : 1];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tid = blockIdx.x * WAVES + wave;
     if (tid >= a.n_tasks) return;   // wave-uniform; no workgroup barriers below
@@ -1388,9 +1402,17 @@ __global__ __launch_bounds__(64 * WAVES, 2) void als_solve_dual(SolveArgs a) {
     float rhs[CD];
 #pragma unroll
     for (int b = 0; b < CD; ++b) rhs[b] = g == 0 ? rr[b] : 0.f;
-    RegTiles<CD> T{acc};
-    RegStore<CD> A0;
-    solve_tiles<CD, true>(T, A0, rhs, buf, tk, a, lane);
+    if constexpr (tiles_in_lds<CD>()) {   // CD = 6: 21 working tiles in per-wave LDS, as the KP = 128 primal solve
+        LdsTiles T{tiles_lds[wave] + (CFK_LDS_B128 ? 4 : 1) * lane};
+        RegStore<CD> A0;
+#pragma unroll
+        for (int p = 0; p < Acc::NT; ++p) T.put(p, acc[p]);
+        solve_tiles<CD, true>(T, A0, rhs, buf, tk, a, lane);
+    } else {
+        RegTiles<CD> T{acc};
+        RegStore<CD> A0;
+        solve_tiles<CD, true>(T, A0, rhs, buf, tk, a, lane);
+    }
     wave_sync();
     // m = Y^T alpha: lane l owns features l + 64 f; entries with alpha = 0 (padding, or exactly 0) are skipped
     float xo[NF];
@@ -1692,6 +1714,7 @@ hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s) {
     if (kp == 64 && cd == 2) als_solve_dual<64, 2><<<grid, 64 * WAVES, 0, s>>>(a);
     else if (kp == 128 && cd == 2) als_solve_dual<128, 2><<<grid, 64 * WAVES, 0, s>>>(a);
     else if (kp == 128 && cd == 4) als_solve_dual<128, 4><<<grid, 64 * WAVES, 0, s>>>(a);
+    else if (kp == 128 && cd == 6) als_solve_dual<128, 6><<<grid, 64 * WAVES, 0, s>>>(a);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }
