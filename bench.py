@@ -214,17 +214,23 @@ def main():
             i = info[side]
             path = eng.block_path(si)
             blocks = eng.block_stats(si)["nnz_padded"] // 32
+            dual = path.get("dual_rows_by_blocks", [0, 0, 0])
+            main_blocks = blocks - sum((c + 1) * n for c, n in enumerate(dual))
+            dual_mfma = sum(n * (cd * (cd + 1) // 2) * (kp // 32) * 6 for n, cd in zip(dual, (2, 4, 6)))
             b = half_bytes(i["nnz"], i["n_rows"], args.k)
             gram_f, solve_f = half_flops(i["nnz"], i["n_rows"], args.k)
             t_s = g_ms[side] / 1000.0
-            mf = blocks * mfma_per_block(kp, path["presplit"]) * MFMA_BF16_FLOP if path["gram_path"] == "mfma_split" else 0
+            mf = ((main_blocks * mfma_per_block(kp, path["presplit"]) + dual_mfma) * MFMA_BF16_FLOP
+                  if path["gram_path"] == "mfma_split" else 0)
             achieved = b / t_s / 1e9
             per[side] = {
-                "kernel": f"als_solve_mfma<{kp},2,split,{'presplit' if path['presplit'] else 'on-the-fly split'}>",
+                "kernel": f"als_solve_mfma<{kp},{1 if kp == 128 else 2},split,"
+                          f"{'presplit' if path['presplit'] else 'on-the-fly split'}> + als_solve_dual (short rows)",
                 "avg_launch_ms": g_ms[side], "reduce_launch_ms": r_ms[side],
                 "algorithmic_bytes": b, "achieved": achieved, "frac": achieved / HBM_PEAK_GBS,
                 "traffic": (tr or {}).get("per_side", {}).get(side),
                 "alg_gram_tflops": gram_f / t_s / 1e12, "alg_solve_tflop_per_launch": solve_f / 1e12,
+                "short_rows_entry_space": dual,
                 "mfma_bf16": {"per_32_entry_block": mfma_per_block(kp, path["presplit"]),
                               "executed_tflops": mf / t_s / 1e12, "peak": BF16_MFMA_PEAK_TFS,
                               "frac": mf / t_s / 1e12 / BF16_MFMA_PEAK_TFS},

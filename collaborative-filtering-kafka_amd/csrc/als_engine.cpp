@@ -1118,7 +1118,8 @@ int als_block_path(const als_engine* e, int side, int* gram_path, int* presplit,
     if (gram_path) *gram_path = (int)e->path;
     if (presplit) *presplit = b.presplit ? 1 : 0;
     if (chunk) *chunk = b.set ? chunk_entries(b.nnz_padded) : 0;
-    if (n_dual_rows) *n_dual_rows = b.n_dual[0] + b.n_dual[1] + b.n_dual[2];
+    if (n_dual_rows)
+        for (int c = 0; c < 3; ++c) n_dual_rows[c] = b.n_dual[c];
     return ALS_OK;
 }
 

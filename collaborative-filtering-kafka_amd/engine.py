@@ -409,10 +409,10 @@ class ALSEngine:
 
     def block_path(self, side) -> dict:
         """Gram variant of the side's block: gram_path ('valu' | 'mfma_f32' | 'mfma_split'), presplit, chunk."""
-        g, p, c, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64()
-        call("als_block_path", self._h, _side(side), ctypes.byref(g), ctypes.byref(p), ctypes.byref(c), ctypes.byref(d))
+        g, p, c, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64(), (ctypes.c_int64 * 3)()
+        call("als_block_path", self._h, _side(side), ctypes.byref(g), ctypes.byref(p), ctypes.byref(c), d)
         return {"gram_path": ("valu", "mfma_f32", "mfma_split")[g.value], "presplit": bool(p.value), "chunk": c.value,
-                "dual_rows": d.value}
+                "dual_rows": sum(d), "dual_rows_by_blocks": list(d)}
 
     def block_stats(self, side):
         a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()

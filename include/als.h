@@ -172,8 +172,9 @@ int als_timing_collect(als_engine* e, int side, double* ms_gram, double* ms_redu
 int als_debug_copy_partials(als_engine* e, void* host_dst, int64_t max_bytes, int64_t* bytes);
 /* Gram variant of `side`'s block: gram_path 0 = LDS-staged VALU (fp64, fp32 k < 32), 1 = fp32 MFMA
  * (v_mfma_f32_16x16x4_f32), 2 = split-bf16 MFMA; presplit = 1 when the opposite table is gathered as pre-split
- * bf16 pieces (RHS on the MFMAs too); chunk = entries per PARTIAL task of a split row; n_dual_rows = short rows
- * solved in entry space, (Y Y^T + lambda n I) alpha = r, m = Y^T alpha (same solution as the k x k system). */
+ * bf16 pieces (RHS on the MFMAs too); chunk = entries per PARTIAL task of a split row; n_dual_rows[3] = short rows
+ * of 1, 2 and 3 padded blocks solved in entry space, (Y Y^T + lambda n I) alpha = r, m = Y^T alpha (the same
+ * solution as the k x k system). */
 int als_block_path(const als_engine* e, int side, int* gram_path, int* presplit, int64_t* chunk, int64_t* n_dual_rows);
 /* Work-plan statistics of the uploaded block (tasks, partial slots, padded nnz). */
 int als_block_stats(const als_engine* e, int side, int64_t* n_tasks, int64_t* n_reduce, int64_t* nnz_padded);
