@@ -385,6 +385,11 @@ __device__ __forceinline__ f32x4 mfma_k32(const u32x4& a, const u32x4& b, f32x4 
 #ifndef CFK_RHS_EARLY
 #define CFK_RHS_EARLY 1
 #endif
+// KP = 128 split Gram: split VALU interleaved into the MFMA issue gaps (column-order tiles), or (0) the plain
+// split_step of the other widths.
+#ifndef CFK_K128_INTERLEAVE
+#define CFK_K128_INTERLEAVE 1
+#endif
 // The solve's v_mfma_f32_16x16x4_f32 groups get the same treatment when CFK_SOLVE_DRAIN is set.
 #ifndef CFK_SOLVE_DRAIN
 #define CFK_SOLVE_DRAIN 0
@@ -877,13 +882,19 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
         for (int s = 0; s < tk.nsteps; ++s) {
             const float* src = part + (int64_t)(tk.slot + s) * (SLOT_WORDS * 64) + lane;
             SlotCodec cd{slot_key(a.gen, tk.slot + s, lane)};
+            // the whole slot's loads are issued before the first use: left to the scheduler under the KP = 128
+            // register pressure they went out one at a time (load, wait, add: 0.44 ms for 974 rows)
+            float w[SLOT_WORDS];
+#pragma unroll
+            for (int q = 0; q < SLOT_WORDS; ++q) w[q] = src[q * 64];
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int p = 0; p < Acc::NT; ++p)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc.g[p][r] += cd.dec(src[(p * 4 + r) * 64], p * 4 + r);
+                for (int r = 0; r < 4; ++r) acc.g[p][r] += cd.dec(w[p * 4 + r], p * 4 + r);
 #pragma unroll
-            for (int c = 0; c < C; ++c) acc.rhs[c] += cd.dec(src[(Acc::NT * 4 + c) * 64], Acc::NT * 4 + c);
-            const bool ok = cd.check_ok(src[Acc::NWORDS * 64], Acc::NWORDS);
+            for (int c = 0; c < C; ++c) acc.rhs[c] += cd.dec(w[Acc::NT * 4 + c], Acc::NT * 4 + c);
+            const bool ok = cd.check_ok(w[Acc::NWORDS], Acc::NWORDS);
             if (!ok && !bad) bad_slot = tk.slot + s;
             bad |= !ok;
         }
@@ -1145,7 +1156,104 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             // Two blocks per trip with ping-pong buffers (no register rotation): column indices are loaded two
             // blocks ahead of their gathers' use, gathers and ratings one block ahead of their MFMAs.
             // Invariant at the loop top: Y0/R0 in flight for block b, I1 = columns of b+1, I0 = columns of b+2.
-            if (C > 4 && nblk > 0) {
+            if (C > 4 && CFK_K128_INTERLEAVE && nblk > 0) {
+                // KP = 128, one wave per SIMD: no second wave hides the split VALU behind this wave's MFMAs, so
+                // the wave interleaves them itself. The tiles are issued column by column (column c = tiles
+                // (b1 <= c, c): 6c + 4 MFMAs), and the split of feature block c + 1 -- the only new operand
+                // column c + 1 needs -- plus a share of the RHS FMAs run in the issue gaps of column c's MFMAs
+                // (an MFMA holds vector issue for 8 of its 16 cycles: two VALU per gap). Column 7's gaps split
+                // feature block 0 of the next block. No operand register dies before column 7 and all of them
+                // are kept allocated past the closing drain (keep_alive), so no VALU result can land in a
+                // register an MFMA in flight still reads. Same products, same accumulation order per tile and
+                // per RHS component as split_step: bitwise equal results.
+                Cols I0, I1;
+                Rats R0, R1;
+                VT Y0[B], Y1[B];
+                u32x4 H[C], M[C], L[C];
+                const int lastb = nblk - 1;
+                auto split_feat = [&](const VT (&y)[B], int c, u32x4& h4, u32x4& m4, u32x4& l4) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        unsigned h, m, l;
+                        split3(y[2 * q][c], y[2 * q + 1][c], h, m, l);
+                        h4[q] = h;
+                        m4[q] = m;
+                        l4[q] = l;
+                    }
+                };
+                auto keep_alive = [&]() {
+#pragma unroll
+                    for (int b = 0; b < C; ++b) asm volatile("" ::"v"(H[b]), "v"(M[b]), "v"(L[b]));
+                };
+                // one block: y/x = this block, yn = the next block (its feature block 0 is split here) when NEXT
+                auto block = [&](const VT (&y)[B], const Rats& x, const VT (&yn)[B], auto next_) {
+                    constexpr bool NEXT = decltype(next_)::value;
+                    u32x4 hn, mn, ln;
+                    static_for<0, C>([&](auto C_) {
+                        constexpr int c = decltype(C_)::value;
+#pragma unroll
+                        for (int b1 = 0; b1 <= c; ++b1) {
+                            f32x4 t = acc.g[tile_index<C>(b1, c)];
+                            t = mfma_k32(M[b1], M[c], t);
+                            if (CFK_DIAG_SYM && b1 == c) {
+                                f32x4 e = E[b1];
+                                e = mfma_k32(H[b1], L[b1], e);
+                                e = mfma_k32(H[b1], M[b1], e);
+                                E[b1] = e;
+                            } else {
+                                t = mfma_k32(H[b1], L[c], t);
+                                t = mfma_k32(L[b1], H[c], t);
+                                t = mfma_k32(H[b1], M[c], t);
+                                t = mfma_k32(M[b1], H[c], t);
+                            }
+                            t = mfma_k32(H[b1], H[c], t);
+                            acc.g[tile_index<C>(b1, c)] = t;
+                        }
+                        if constexpr (c + 1 < C) split_feat(y, c + 1, H[c + 1], M[c + 1], L[c + 1]);
+                        // RHS components 0-1 in column 5's gaps, 2-4 in column 6's, 5-7 in column 7's
+                        constexpr int r0 = c == 5 ? 0 : c == 6 ? 2 : c == 7 ? 5 : C;
+                        constexpr int r1 = c == 5 ? 2 : c == 6 ? 5 : c == 7 ? 8 : C;
+#pragma unroll
+                        for (int f = r0; f < r1; ++f)
+#pragma unroll
+                            for (int t = 0; t < B; ++t) acc.rhs[f] += x.r[t >> 2][t & 3] * y[t][f];
+                        if constexpr (NEXT && c == C - 1) split_feat(yn, 0, hn, mn, ln);
+                        static_for<0, 6 * c + 4>([&](auto) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+                            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // 2 VALU
+                        });
+                        __builtin_amdgcn_sched_barrier(0);
+                    });
+                    MFMA_DRAIN();
+                    keep_alive();
+                    __builtin_amdgcn_sched_barrier(0);
+                    if constexpr (NEXT) {
+                        H[0] = hn;
+                        M[0] = mn;
+                        L[0] = ln;
+                    }
+                };
+                using Yes = std::integral_constant<bool, true>;
+                using No = std::integral_constant<bool, false>;
+                // one block per trip, staging rotated (two blocks per trip with ping-pong buffers made the
+                // register allocator shuffle the 144 accumulator registers at every back edge)
+                load_cols(0, I0);
+                load_cols(min(1, lastb), I1);
+                gather_blk(I0, Y0);
+                load_rats(0, R0);
+                split_feat(Y0, 0, H[0], M[0], L[0]);
+                for (int b = 0; b < lastb; ++b) {
+                    gather_blk(I1, Y1);
+                    load_rats(b + 1, R1);
+                    load_cols(min(b + 2, lastb), I1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    block(Y0, R0, Y1, Yes{});
+#pragma unroll
+                    for (int t = 0; t < B; ++t) Y0[t] = Y1[t];
+                    R0 = R1;
+                }
+                block(Y0, R0, Y1, No{});
+            } else if (C > 4 && nblk > 0) {
                 // KP = 128 (1 wave per SIMD, 144 accumulator registers): one staging set, rotated
                 Cols Ic, In;
                 Rats Rc, Rn;
