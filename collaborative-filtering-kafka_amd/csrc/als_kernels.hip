@@ -830,6 +830,11 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 template <int KP>
 constexpr int mfma_waves() { return WAVES; }
 
+// Pre-split row layout: [h,m pieces][l pieces] (1: contiguous gathers for a 16-lane group) or [h,m,l] per 24-B
+// piece (0).
+#ifndef CFK_PRESPLIT_HML
+#define CFK_PRESPLIT_HML 1
+#endif
 // fp32 table -> bf16 h/m/l pieces (PRESPLIT_ROW_BYTES per row), one thread per 16-B row piece.
 __global__ __launch_bounds__(256) void als_presplit(const float* __restrict__ src, unsigned* __restrict__ dst,
                                                    int64_t n_pieces) {
@@ -839,10 +844,19 @@ __global__ __launch_bounds__(256) void als_presplit(const float* __restrict__ sr
     unsigned h01, m01, l01, h23, m23, l23;
     split3(x[0], x[1], h01, m01, l01);
     split3(x[2], x[3], h23, m23, l23);
-    unsigned* o = dst + t * 6;
-    *(u32x2*)o = u32x2{h01, h23};
-    *(u32x2*)(o + 2) = u32x2{m01, m23};
-    *(u32x2*)(o + 4) = u32x2{l01, l23};
+    if constexpr (CFK_PRESPLIT_HML) {
+        // row = [h, m of 16 pieces: 16 x 16 B][l of 16 pieces: 16 x 8 B], so both gathers of a 16-lane group
+        // are contiguous (16-B and 8-B lane strides)
+        unsigned* o = dst + (t >> 4) * (PRESPLIT_ROW_BYTES / 4);
+        const int j = (int)(t & 15);
+        *(u32x4*)(o + 4 * j) = u32x4{h01, h23, m01, m23};
+        *(u32x2*)(o + 64 + 2 * j) = u32x2{l01, l23};
+    } else {
+        unsigned* o = dst + t * 6;
+        *(u32x2*)o = u32x2{h01, h23};
+        *(u32x2*)(o + 2) = u32x2{m01, m23};
+        *(u32x2*)(o + 4) = u32x2{l01, l23};
+    }
 }
 
 // REDUCE = true: the launch of a half's REDUCE tasks (sum of partial slots + solve), compiled apart from the
@@ -961,16 +975,24 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                 x.r[0] = *(const f32x4*)r;
                 x.r[1] = *(const f32x4*)(r + 4);
             };
-            const char* sbase = (const char*)a.opp_split + j * 24;
+            const char* sbase = (const char*)a.opp_split + (CFK_PRESPLIT_HML ? j * 16 : j * 24);
             auto gather_blk = [&](const Cols& x, Piece (&y)[B]) {
 #pragma unroll
                 for (int t = 0; t < B; ++t) {
                     // 24-bit multiply (full rate; pre-split tables are small: host-checked < 2^24 rows)
                     const char* p = sbase + __umul24((uint32_t)x.i[t >> 2][t & 3], (uint32_t)PRESPLIT_ROW_BYTES);
-                    const u32x2 a0 = *(const u32x2*)p, a1 = *(const u32x2*)(p + 8), a2 = *(const u32x2*)(p + 16);
-                    y[t].w[0] = a0[0]; y[t].w[1] = a0[1];
-                    y[t].w[2] = a1[0]; y[t].w[3] = a1[1];
-                    y[t].w[4] = a2[0]; y[t].w[5] = a2[1];
+                    if constexpr (CFK_PRESPLIT_HML) {
+                        const u32x4 hm = *(const u32x4*)p;
+                        const u32x2 l = *(const u32x2*)(p + 256 - 8 * j);   // l piece j at 256 + 8 j
+                        y[t].w[0] = hm[0]; y[t].w[1] = hm[1];
+                        y[t].w[2] = hm[2]; y[t].w[3] = hm[3];
+                        y[t].w[4] = l[0]; y[t].w[5] = l[1];
+                    } else {
+                        const u32x2 a0 = *(const u32x2*)p, a1 = *(const u32x2*)(p + 8), a2 = *(const u32x2*)(p + 16);
+                        y[t].w[0] = a0[0]; y[t].w[1] = a0[1];
+                        y[t].w[2] = a1[0]; y[t].w[3] = a1[1];
+                        y[t].w[4] = a2[0]; y[t].w[5] = a2[1];
+                    }
                 }
             };
             f32x4 racc[C];
