@@ -115,6 +115,11 @@ struct als_engine {
     hipEvent_t solved = nullptr;         // recorded on `stream` before each all-gather
     hipEvent_t gathered[2] = {nullptr, nullptr};   // last all-gather of each side, on comm_stream
     bool gather_pending[2] = {false, false};
+    // Entry-space (als_solve_dual) launches run on side_stream, forked from and joined back into `stream`, so
+    // they fill the CUs the main launch's tail leaves idle (ALS_DUAL_SIDE=0: same stream, after the main launch)
+    bool dual_side = true;
+    hipStream_t side_stream = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     std::vector<TimingRec> pending;
@@ -244,6 +249,7 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
     if (const char* env = getenv("ALS_DEBUG_REDUCE_GEN_SKEW")) e->debug_gen_skew = (uint32_t)atoi(env);
     if (const char* env = getenv("ALS_DEBUG_FIXED_GEN")) e->debug_fixed_gen = env[0] == '1';
     if (const char* env = getenv("ALS_REFINE_MIN_PIVOT")) e->refine_min_pivot = (float)atof(env);
+    if (const char* env = getenv("ALS_DUAL_SIDE")) e->dual_side = env[0] != '0';
     if (const char* env = getenv("ALS_DEBUG_SKIP_REFINE"))
         if (env[0] == '1') e->debug_flags |= cfk::SOLVE_FLAG_SKIP_REFINE;
     hipError_t st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
@@ -282,6 +288,12 @@ int als_engine_destroy(als_engine* e) {
     if (e->comm) (void)ncclCommDestroy(e->comm);
     if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
     for (auto ev : {e->solved, e->gathered[0], e->gathered[1]})
+        if (ev) (void)hipEventDestroy(ev);
+    if (e->side_stream) {
+        (void)hipStreamSynchronize(e->side_stream);
+        (void)hipStreamDestroy(e->side_stream);
+    }
+    for (auto ev : {e->fork, e->join})
         if (ev) (void)hipEventDestroy(ev);
     if (e->own_stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -746,18 +758,33 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
         }
         HIP_TRY(hipEventRecord(rec.ev[0], e->stream));
     }
+    const bool any_dual = dl.n[0] > 0 || dl.n[1] > 0 || dl.n[2] > 0;
+    const bool side_dual = any_dual && e->dual_side;
+    if (side_dual) {   // the dual launches read the fp32 opposite table only: fork before the pre-split
+        if (!e->side_stream) {
+            HIP_TRY(hipStreamCreateWithFlags(&e->side_stream, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&e->fork, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&e->join, hipEventDisableTiming));
+        }
+        HIP_TRY(hipEventRecord(e->fork, e->stream));
+    }
     if (b.presplit) {
         HIP_TRY(cfk::launch_presplit((const float*)opp.ptr, e->d_split, b.n_opp_rows + 1, e->stream));
         a.opp_split = e->d_split;
     }
     HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves, b.presplit, false));
+    if (side_dual) HIP_TRY(hipStreamWaitEvent(e->side_stream, e->fork, 0));
     for (int c = 0; c < 3; ++c)
         if (dl.n[c] > 0) {
             cfk::SolveArgs d = a;
             d.tasks = dl.t[c];
             d.n_tasks = dl.n[c];
-            HIP_TRY(cfk::launch_dual(e->kp, 2 * (c + 1), d, e->stream));
+            HIP_TRY(cfk::launch_dual(e->kp, 2 * (c + 1), d, side_dual ? e->side_stream : e->stream));
         }
+    if (side_dual) {
+        HIP_TRY(hipEventRecord(e->join, e->side_stream));
+        HIP_TRY(hipStreamWaitEvent(e->stream, e->join, 0));
+    }
     if (e->timing) HIP_TRY(hipEventRecord(rec.ev[1], e->stream));
     if (n_reduce > 0) {
         a.tasks = reduce;
