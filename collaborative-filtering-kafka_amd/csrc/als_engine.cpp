@@ -769,7 +769,10 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
         HIP_TRY(hipEventRecord(e->fork, e->stream));
     }
     if (b.presplit) {
-        HIP_TRY(cfk::launch_presplit((const float*)opp.ptr, e->d_split, b.n_opp_rows + 1, e->stream));
+        // the opposite replica is the half's input and does not change between its chunks (als.h): chunk 0
+        // converts it, later chunks reuse the conversion
+        if (first_chunk)
+            HIP_TRY(cfk::launch_presplit((const float*)opp.ptr, e->d_split, b.n_opp_rows + 1, e->stream));
         a.opp_split = e->d_split;
     }
     HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves, b.presplit, false));

@@ -116,7 +116,9 @@ int als_solve_half(als_engine* e, int side, float lambda);
  * ranges of its local rows, row_bounds[0] = 0 <= ... <= row_bounds[n_chunks] = n_rows; the union of the
  * chunk launches is exactly als_solve_half. Lets the caller all-gather chunk c of the updated shard over
  * RCCL while chunk c+1 is solved -- the per-partition fan-out of the reference's feature topics
- * (ALSApp.java:105-148) overlapped with compute. Replaces any previous chunking of that side. */
+ * (ALSApp.java:105-148) overlapped with compute. Replaces any previous chunking of that side. The chunks of
+ * one half are solved in ascending order starting with chunk 0, and the opposite factor replica (the half's
+ * input) does not change between them: chunk 0 prepares it (the pre-split copy), later chunks reuse that. */
 int als_set_chunks(als_engine* e, int side, int n_chunks, const int64_t* row_bounds);
 int als_solve_half_chunk(als_engine* e, int side, float lambda, int chunk);
 
