@@ -119,7 +119,7 @@ def cpu_baseline(ds, k, lam, seconds, thread_counts):
 
 
 def load_traffic(k, nnz):
-    path = os.path.join(ROOT, "profiles", "traffic.json")
+    path = os.path.join(ROOT, "profiles", "traffic.json" if k == 64 else f"traffic_k{k}.json")
     try:
         tr = json.load(open(path))
     except (OSError, ValueError):

@@ -9,7 +9,7 @@ Writes:
                               KiB -> B, FETCH doubled on gfx950), and the SQ counters of the full launch and of
                               the Gram alone (ALS_DEBUG_SKIP_SOLVE=1): MFMA busy share, issue stalls, clock
   bench_line.json             the bench.py line of the same call
-and profiles/traffic.json (read by bench.py: per_side HBM bytes per launch).
+and profiles/traffic.json (k = 64) or traffic_k<k>.json (read by bench.py: per_side HBM bytes per launch).
 Sides: the main solve kernel dispatch with the largest grid is the user half (480,189 tasks), the next the movie
 half (FULL + PARTIAL tasks); the REDUCE kernel instantiation is recognised by its last template argument.
 
@@ -119,11 +119,13 @@ def main(tag, name):
             open(os.path.join(dst, "bench_line.json"), "w").write(line[-1])
     bench = json.loads(open(os.path.join(dst, "bench_line.json")).read()) if os.path.exists(os.path.join(dst, "bench_line.json")) else {}
     cfg = bench.get("config", {})
-    json.dump({"k": cfg.get("k", 64), "nnz": cfg.get("nnz", 100_000_000),
+    k = cfg.get("k", 64)
+    tname = "traffic.json" if k == 64 else f"traffic_k{k}.json"
+    json.dump({"k": k, "nnz": cfg.get("nnz", 100_000_000),
                "per_side": {s: traffic[s]["hbm_bytes"] for s in ("movie", "user") if s in traffic},
                "detail": traffic, "source": f"profiles/{name}",
                "note": "per launch: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> B; Infinity-Cache hits "
-                       "are counted by these counters"}, open(os.path.join(ROOT, "profiles", "traffic.json"), "w"),
+                       "are counted by these counters"}, open(os.path.join(ROOT, "profiles", tname), "w"),
               indent=1)
     print(json.dumps({k: out[k] for k in ("trace", "traffic")}, indent=1))
 
