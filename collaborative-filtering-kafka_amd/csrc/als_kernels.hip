@@ -835,6 +835,12 @@ constexpr int mfma_waves() { return WAVES; }
 #ifndef CFK_PRESPLIT_HML
 #define CFK_PRESPLIT_HML 1
 #endif
+// Pre-split Gram: a block's 32 column indices and 32 ratings come with ONE 4-B load per lane (lane (g, j < 8):
+// column of entry 8g + j, lane (g, j >= 8): its rating) and reach the 16 lanes of group g by DPP row_newbcast (1),
+// instead of four 16-B loads per lane that every lane of a group issues for the same 8 entries (0).
+#ifndef CFK_PRESPLIT_CR
+#define CFK_PRESPLIT_CR 1
+#endif
 // fp32 table -> bf16 h/m/l pieces (PRESPLIT_ROW_BYTES per row), one thread per 16-B row piece.
 __global__ __launch_bounds__(256) void als_presplit(const float* __restrict__ src, unsigned* __restrict__ dst,
                                                    int64_t n_pieces) {
@@ -998,7 +1004,22 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             f32x4 racc[C];
 #pragma unroll
             for (int b = 0; b < C; ++b) racc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-            auto step = [&](const Piece (&y)[B], const Rats& x) {
+            // CFK_PRESPLIT_CR: one 4-B load per lane and block, expanded by DPP broadcasts inside the group
+            const int32_t* crb = (j < 8 ? a.col : (const int32_t*)a.rat) + tk.begin + g * B + (j & 7);
+            auto load_cr = [&](int blk) { return crb[(int64_t)blk * BLOCK_ENTRIES]; };
+            auto expand_cr = [&](int v, Cols& I, u32x4& R) {
+                static_for<0, 8>([&](auto T) {
+                    constexpr int t = T;
+                    I.i[t >> 2][t & 3] = __builtin_amdgcn_mov_dpp(v, 0x150 + t, 0xf, 0xf, false);
+                });
+                static_for<0, 4>([&](auto Q) {
+                    constexpr int q = Q;
+                    const float r0 = __int_as_float(__builtin_amdgcn_mov_dpp(v, 0x150 + 8 + 2 * q, 0xf, 0xf, false));
+                    const float r1 = __int_as_float(__builtin_amdgcn_mov_dpp(v, 0x150 + 9 + 2 * q, 0xf, 0xf, false));
+                    R[q] = pk_bf16(r0, r1);
+                });
+            };
+            auto step = [&](const Piece (&y)[B], const auto& x) {
                 u32x4 P[3][C];   // plane (h, m, l) x feature block b: entries 0..7 as bf16 pairs
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl)
@@ -1015,7 +1036,11 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                 u32x4 R;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    unsigned v = pk_bf16(x.r[q >> 1][2 * (q & 1)], x.r[q >> 1][2 * (q & 1) + 1]);
+                    unsigned v;
+                    if constexpr (std::is_same_v<std::decay_t<decltype(x)>, Rats>)
+                        v = pk_bf16(x.r[q >> 1][2 * (q & 1)], x.r[q >> 1][2 * (q & 1) + 1]);
+                    else
+                        v = x[q];   // packed by expand_cr
                     pin(v);
                     R[q] = v;
                 }
@@ -1050,7 +1075,43 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                 }
                 MFMA_DRAIN();
             };
-            if (nblk > 0) {
+            if constexpr (CFK_PRESPLIT_CR) {
+              if (nblk > 0) {
+                // same pipeline as below: loads two blocks ahead of their gathers' use, gathers one block ahead
+                Cols I;
+                u32x4 R0, R1;
+                Piece Y0[B], Y1[B];
+                const int lastb = nblk - 1;
+                int v0 = load_cr(0), v1 = load_cr(min(1, lastb));
+                expand_cr(v0, I, R0);
+                gather_blk(I, Y0);
+                v0 = load_cr(min(2, lastb));
+                int b = 0;
+                for (; b + 2 < nblk; b += 2) {
+                    expand_cr(v1, I, R1);
+                    gather_blk(I, Y1);
+                    v1 = load_cr(min(b + 3, lastb));
+                    __builtin_amdgcn_sched_barrier(0);
+                    step(Y0, R0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    expand_cr(v0, I, R0);
+                    gather_blk(I, Y0);
+                    v0 = load_cr(min(b + 4, lastb));
+                    __builtin_amdgcn_sched_barrier(0);
+                    step(Y1, R1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (nblk - b == 2) {
+                    expand_cr(v1, I, R1);
+                    gather_blk(I, Y1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    step(Y0, R0);
+                    step(Y1, R1);
+                } else {
+                    step(Y0, R0);
+                }
+              }
+            } else if (nblk > 0) {
                 Cols I0, I1;
                 Rats R0, R1;
                 Piece Y0[B], Y1[B];

@@ -1,8 +1,8 @@
 set -u
-S=tools/gpu_step.sh
 B=collaborative-filtering-kafka_amd
-CFK_ALS_LIB=$B/build_treg0/libcfk_als.so $S 300 dump_old.log python -u tools/dump_iteration.py --k 128 --out /tmp/old.npz || exit 1
-CFK_ALS_LIB=$B/build/libcfk_als.so $S 300 dump_new.log python -u tools/dump_iteration.py --k 128 --out /tmp/new.npz || exit 1
-$S 120 cmp.log python -u tools/dump_iteration.py --compare /tmp/old.npz /tmp/new.npz
-rm -f /tmp/old.npz /tmp/new.npz
-timeout -k 10 600 bash tools/ab_builds.sh "build build_treg0" "--k 128 --rounds 3 --variants ALS_DUAL=1 ALS_DUAL=0" 2 || exit 1
+tools/gpu_step.sh 300 t_cr.log python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullscale.py -m gpu -x -q --timeout 250 --timeout-method thread -k "every_k or extreme or split or determinism or fullscale or full" || exit 1
+grep -q "passed" gpurun_out/t_cr.log || exit 1
+tools/gpu_step.sh 200 d1.log python tools/dump_iteration.py --k 64 --out gpurun_out/cr1.npz || exit 1
+CFK_ALS_LIB=$B/build_cr0/libcfk_als.so tools/gpu_step.sh 200 d0.log python tools/dump_iteration.py --k 64 --out gpurun_out/cr0.npz || exit 1
+python tools/dump_iteration.py --compare gpurun_out/cr0.npz gpurun_out/cr1.npz
+tools/ab_builds.sh "build build_cr0" "--rounds 5" 3
