@@ -100,6 +100,7 @@ struct als_engine {
     uint32_t* d_integrity = nullptr;   // cfk::INTEGRITY_WORDS: partial slots that failed their check
     uint32_t gen = 0;               // launch generation of the next PARTIAL/REDUCE pair
     int min_waves = 0;              // ALS_MFMA_WAVES override of the per-block occupancy choice (0 = auto)
+    int split_waves = 2;            // ALS_SPLIT_WAVES: waves per SIMD of the on-the-fly split-bf16 variant
     int32_t debug_flags = 0;        // ALS_DEBUG_SKIP_SOLVE=1 -> cfk::SOLVE_FLAG_SKIP_SOLVE (tools/kbench.py only)
     uint32_t debug_gen_skew = 0;    // ALS_DEBUG_REDUCE_GEN_SKEW=n: REDUCE decodes with generation + n (tests the
                                     // integrity check: every slot then reads as written by another launch)
@@ -244,6 +245,7 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
     e->precision = precision;
     e->path = path;
     if (const char* env = getenv("ALS_MFMA_WAVES")) e->min_waves = std::max(0, atoi(env));
+    if (const char* env = getenv("ALS_SPLIT_WAVES")) e->split_waves = std::max(2, atoi(env));
     if (const char* env = getenv("ALS_DEBUG_SKIP_SOLVE"))
         if (env[0] == '1') e->debug_flags |= cfk::SOLVE_FLAG_SKIP_SOLVE;
     if (const char* env = getenv("ALS_DEBUG_REDUCE_GEN_SKEW")) e->debug_gen_skew = (uint32_t)atoi(env);
@@ -459,8 +461,6 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     blk.n_tasks = (int32_t)tasks.size();
     blk.n_reduce = (int32_t)reduce.size();
     blk.n_slots = (int32_t)slots;
-    // 2 waves/SIMD (the split-bf16 path has one variant; the f32 path takes ALS_MFMA_WAVES=3 for experiments)
-    blk.min_waves = e->min_waves > 0 ? e->min_waves : 2;
     // Pre-split opposite table for the split-bf16 Gram when it stays L2-resident (<= 8 MB as h/m/l pieces,
     // e.g. the 17,770-row movie table of the user half): 1.5x the gathered bytes from L2, ~3x fewer VALU
     // instructions per block (measured on the Netflix-shape user half). ALS_PRESPLIT=0/1 forces it.
@@ -473,6 +473,10 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
         // take the fp32 VALU RHS of the on-the-fly split path instead
         if (max_abs_rating > 256) ps = false;
         blk.presplit = ps;
+        // waves per SIMD of the main launch: the pre-split Gram runs 3 (one gather buffer in 168 VGPRs, the
+        // other waves hide its latency: Netflix-shape user half 4.18 -> 3.84 ms, kbench), the other MFMA variants
+        // 2. ALS_MFMA_WAVES overrides all; ALS_SPLIT_WAVES=3 selects the one-buffer variant of the on-the-fly split.
+        blk.min_waves = e->min_waves > 0 ? e->min_waves : (ps ? 3 : e->split_waves);
         if (ps && (size_t)sb > e->split_bytes) {
             (void)hipFree(e->d_split);
             e->d_split = nullptr;

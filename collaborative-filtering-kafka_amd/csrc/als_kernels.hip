@@ -1075,7 +1075,25 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                 }
                 MFMA_DRAIN();
             };
-            if constexpr (CFK_PRESPLIT_CR) {
+            if constexpr (CFK_PRESPLIT_CR && MINW >= 3) {
+                // three waves per SIMD (168 VGPRs): one gather buffer, the other waves hide its latency; the
+                // block's columns/ratings are still loaded one block ahead
+                if (nblk > 0) {
+                    Cols I;
+                    u32x4 R;
+                    Piece Y[B];
+                    const int lastb = nblk - 1;
+                    int v = load_cr(0);
+                    for (int b = 0; b < nblk; ++b) {
+                        expand_cr(v, I, R);
+                        gather_blk(I, Y);
+                        v = load_cr(min(b + 1, lastb));
+                        __builtin_amdgcn_sched_barrier(0);
+                        step(Y, R);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+            } else if constexpr (CFK_PRESPLIT_CR) {
               if (nblk > 0) {
                 // same pipeline as below: loads two blocks ahead of their gathers' use, gathers one block ahead
                 Cols I;
@@ -1358,6 +1376,21 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                     Rc = Rn;
                 }
                 split_step(Yc, Rc);
+            } else if (MINW >= 3 && nblk > 0) {
+                // three waves per SIMD: one gather buffer, columns one block ahead
+                Cols I;
+                Rats R;
+                VT Y[B];
+                const int lastb = nblk - 1;
+                load_cols(0, I);
+                for (int b = 0; b < nblk; ++b) {
+                    gather_blk(I, Y);
+                    load_rats(b, R);
+                    load_cols(min(b + 1, lastb), I);
+                    __builtin_amdgcn_sched_barrier(0);
+                    split_step(Y, R);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             } else if (nblk > 0) {
                 Cols I0, I1;
                 Rats R0, R1;
@@ -1920,7 +1953,10 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA, 1>(a, s, reduce);
         } else if (path == Path::MFMA_SPLIT) {
             if (kp == 32) return launch_solve_t<float, 32, Path::MFMA_SPLIT, 2>(a, s, reduce);
+            if (kp == 64 && presplit && min_waves >= 3)
+                return launch_solve_t<float, 64, Path::MFMA_SPLIT, 3, true>(a, s, reduce);
             if (kp == 64 && presplit) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2, true>(a, s, reduce);
+            if (kp == 64 && min_waves >= 3) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 3>(a, s, reduce);
             if (kp == 64) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2>(a, s, reduce);
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1>(a, s, reduce);
         } else {
