@@ -224,7 +224,7 @@ def main():
                   if path["gram_path"] == "mfma_split" else 0)
             achieved = b / t_s / 1e9
             per[side] = {
-                "kernel": f"als_solve_mfma<{kp},{1 if kp == 128 else 2},split,"
+                "kernel": f"als_solve_mfma<{kp},{1 if kp == 128 else (3 if path['presplit'] else 2)},split,"
                           f"{'presplit' if path['presplit'] else 'on-the-fly split'}> + als_solve_dual (short rows)",
                 "avg_launch_ms": g_ms[side], "reduce_launch_ms": r_ms[side],
                 "algorithmic_bytes": b, "achieved": achieved, "frac": achieved / HBM_PEAK_GBS,
