@@ -943,11 +943,15 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
         };
         // unconditional: padding entries index the sentinel zero row; 32-bit unsigned byte offsets (host-checked:
         // opposite table <= 4 GiB, e.g. 16.7M rows at k = 64)
-        const char* obase = (const char*)(opp + C * j);
+        // wave-uniform table base + 32-bit per-lane byte offsets (row << log2(row bytes), + this lane's piece): the
+        // loads take the saddr form, one v_lshl_add_u32 per gathered row instead of a 64-bit address per lane
+        const char* obase = (const char*)opp;
+        const uint32_t lane_off = (uint32_t)(C * j * sizeof(float));
+        constexpr int ROW_SHIFT = __builtin_ctz(KP * sizeof(float));
         auto gather = [&](const Idx& x, VT (&y)[B]) {
 #pragma unroll
             for (int t = 0; t < B; ++t)
-                y[t] = *(const VT*)(obase + (uint32_t)x.i[t >> 2][t & 3] * (uint32_t)(KP * sizeof(float)));
+                y[t] = *(const VT*)(obase + (((uint32_t)x.i[t >> 2][t & 3] << ROW_SHIFT) + lane_off));
         };
         auto mfma_step = [&](const VT& y, float r) {
 #pragma unroll
@@ -982,14 +986,19 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                 x.r[1] = *(const f32x4*)(r + 4);
             };
             const char* sbase = (const char*)a.opp_split + (CFK_PRESPLIT_HML ? j * 16 : j * 24);
+            const char* tbase = (const char*)a.opp_split;
+            const uint32_t hm_off = 16u * j, l_off = 256u + 8u * j;
             auto gather_blk = [&](const Cols& x, Piece (&y)[B]) {
 #pragma unroll
                 for (int t = 0; t < B; ++t) {
                     // 24-bit multiply (full rate; pre-split tables are small: host-checked < 2^24 rows)
                     const char* p = sbase + __umul24((uint32_t)x.i[t >> 2][t & 3], (uint32_t)PRESPLIT_ROW_BYTES);
                     if constexpr (CFK_PRESPLIT_HML) {
-                        const u32x4 hm = *(const u32x4*)p;
-                        const u32x2 l = *(const u32x2*)(p + 256 - 8 * j);   // l piece j at 256 + 8 j
+                        // wave-uniform table base + 32-bit per-lane offsets (saddr form: one 24-bit multiply-add per
+                        // load instead of a 64-bit address per lane); l piece j at 256 + 8 j
+                        const uint32_t ro = __umul24((uint32_t)x.i[t >> 2][t & 3], (uint32_t)PRESPLIT_ROW_BYTES);
+                        const u32x4 hm = *(const u32x4*)(tbase + (ro + hm_off));
+                        const u32x2 l = *(const u32x2*)(tbase + (ro + l_off));
                         y[t].w[0] = hm[0]; y[t].w[1] = hm[1];
                         y[t].w[2] = hm[2]; y[t].w[3] = hm[3];
                         y[t].w[4] = l[0]; y[t].w[5] = l[1];
@@ -1198,7 +1207,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             auto gather_blk = [&](const Cols& x, VT (&y)[B]) {
 #pragma unroll
                 for (int t = 0; t < B; ++t)
-                    y[t] = *(const VT*)(obase + (uint32_t)x.i[t >> 2][t & 3] * (uint32_t)(KP * sizeof(float)));
+                    y[t] = *(const VT*)(obase + (((uint32_t)x.i[t >> 2][t & 3] << ROW_SHIFT) + lane_off));
             };
             auto split_step = [&](const VT (&y)[B], const Rats& x) {
                 u32x4 H[C], M[C], L[C];
@@ -1435,7 +1444,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                 constexpr int h = decltype(h_)::value;
 #pragma unroll
                 for (int t = 0; t < H; ++t)
-                    y[t] = *(const VT*)(obase + (uint32_t)x.i[h][t] * (uint32_t)(KP * sizeof(float)));
+                    y[t] = *(const VT*)(obase + (((uint32_t)x.i[h][t] << ROW_SHIFT) + lane_off));
             };
             using H0 = std::integral_constant<int, 0>;
             using H1 = std::integral_constant<int, 1>;
