@@ -45,6 +45,7 @@ struct Block {
     int64_t n_rows = 0, row_offset = 0, n_opp_rows = 0, nnz = 0, nnz_padded = 0;
     int32_t* d_col = nullptr;
     float* d_rat = nullptr;
+    uint32_t* d_rat_pk = nullptr;   // pre-split blocks: ratings as bf16 pairs (the Gram's RHS operand)
     Task* d_tasks = nullptr;        // FULL + PARTIAL, sorted by work (longest first)
     Task* d_reduce = nullptr;       // REDUCE
     int32_t n_tasks = 0, n_reduce = 0, n_slots = 0;
@@ -169,6 +170,7 @@ int check_side(int side) {
 void free_block(Block& b) {
     (void)hipFree(b.d_col);
     (void)hipFree(b.d_rat);
+    (void)hipFree(b.d_rat_pk);
     (void)hipFree(b.d_tasks);
     (void)hipFree(b.d_reduce);
     (void)hipFree(b.d_task_se);
@@ -486,6 +488,16 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
                                               hipGetErrorString(st));
             e->split_bytes = (size_t)sb;
         }
+        if (ps && nnz_padded > 0) {
+            // the RHS operand's ratings, packed once (setup time): one 4-B load per lane then carries a block's
+            // columns and its bf16 rating pairs (als_kernels.hip, CFK_PRESPLIT_CR)
+            hipError_t st = hipMalloc((void**)&blk.d_rat_pk, (size_t)nnz_padded * 2);
+            if (st != hipSuccess) return fail(ALS_ERR_OUT_OF_MEMORY, "hipMalloc(%lld): %s", (long long)nnz_padded * 2,
+                                              hipGetErrorString(st));
+            st = cfk::launch_pack_ratings(blk.d_rat, blk.d_rat_pk, nnz_padded / 2, nullptr);
+            if (st == hipSuccess) st = hipDeviceSynchronize();
+            if (st != hipSuccess) return fail(ALS_ERR_DEVICE, "pack ratings: %s", hipGetErrorString(st));
+        }
     }
     auto up = [&](void** dst, const void* src, size_t bytes) -> int {
         if (bytes == 0) return ALS_OK;
@@ -778,6 +790,7 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
         if (first_chunk)
             HIP_TRY(cfk::launch_presplit((const float*)opp.ptr, e->d_split, b.n_opp_rows + 1, e->stream));
         a.opp_split = e->d_split;
+        a.rat_pk = b.d_rat_pk;
     }
     HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves, b.presplit, false));
     if (side_dual) HIP_TRY(hipStreamWaitEvent(e->side_stream, e->fork, 0));

@@ -59,6 +59,7 @@ struct SolveArgs {
     uint32_t gen;           // launch generation (PARTIAL and its REDUCE share it): keys the partial-slot encoding
     uint32_t* integrity;    // device record of partial slots that failed their check (see als_kernels.hip)
     float refine_min_pivot; // MFMA tile solve: skip the refinement step when every scaled pivot >= this (> 1: never)
+    const uint32_t* rat_pk; // presplit: the padded ratings as bf16 pairs (entries 2i, 2i+1), exact for |r| <= 256
 };
 // Partial-slot integrity record (device, 4 words): [0] REDUCE tasks that found a bad slot, [1] generation, [2] slot,
 // [3] row of the first failure. Read back by every synchronising call of the engine.
@@ -98,6 +99,8 @@ hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s);
 // h(f0,f1) h(f2,f3) m(f0,f1) m(f2,f3) l(f0,f1) l(f2,f3).
 constexpr int PRESPLIT_ROW_BYTES = 384;
 hipError_t launch_presplit(const float* src, void* dst, int64_t n_rows, hipStream_t s);
+// padded fp32 ratings -> bf16 pairs (n_pairs = nnz_padded / 2)
+hipError_t launch_pack_ratings(const float* rat, uint32_t* dst, int64_t n_pairs, hipStream_t s);
 // bytes % 16 == 0; host_pinned must stay valid until the stream has passed the copy
 hipError_t launch_upload(const void* host_pinned, void* dst, size_t bytes, hipStream_t s);
 hipError_t launch_download(const void* src, void* host_pinned, size_t bytes, hipStream_t s);

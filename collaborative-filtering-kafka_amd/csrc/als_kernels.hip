@@ -1014,8 +1014,12 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
 #pragma unroll
             for (int b = 0; b < C; ++b) racc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
             // CFK_PRESPLIT_CR: one 4-B load per lane and block, expanded by DPP broadcasts inside the group
-            const int32_t* crb = (j < 8 ? a.col : (const int32_t*)a.rat) + tk.begin + g * B + (j & 7);
-            auto load_cr = [&](int blk) { return crb[(int64_t)blk * BLOCK_ENTRIES]; };
+            // lane (g, j < 8): column of entry 8g + j; lane (g, 8 + q): bf16 rating pair (8g + 2q, 8g + 2q + 1)
+            // (lanes 12..15 repeat pairs 0..3)
+            const int32_t* crb = j < 8 ? a.col + tk.begin + g * B + j
+                                       : (const int32_t*)a.rat_pk + (tk.begin >> 1) + g * 4 + (j & 3);
+            const int cshift = j < 8 ? 5 : 4;   // per-block stride: 32 columns or 16 rating pairs
+            auto load_cr = [&](int blk) { return crb[blk << cshift]; };
             auto expand_cr = [&](int v, Cols& I, u32x4& R) {
                 static_for<0, 8>([&](auto T) {
                     constexpr int t = T;
@@ -1023,9 +1027,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                 });
                 static_for<0, 4>([&](auto Q) {
                     constexpr int q = Q;
-                    const float r0 = __int_as_float(__builtin_amdgcn_mov_dpp(v, 0x150 + 8 + 2 * q, 0xf, 0xf, false));
-                    const float r1 = __int_as_float(__builtin_amdgcn_mov_dpp(v, 0x150 + 9 + 2 * q, 0xf, 0xf, false));
-                    R[q] = pk_bf16(r0, r1);
+                    R[q] = (unsigned)__builtin_amdgcn_mov_dpp(v, 0x150 + 8 + q, 0xf, 0xf, false);
                 });
             };
             auto step = [&](const Piece (&y)[B], const auto& x) {
@@ -1934,6 +1936,16 @@ hipError_t launch_download(const void* src, void* host_pinned, size_t bytes, hip
     return launch_copy(src, host_pinned, bytes, 1, s);
 }
 
+__global__ __launch_bounds__(256) void als_pack_ratings(const float* __restrict__ rat, uint32_t* __restrict__ dst,
+                                                        int64_t n_pairs) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n_pairs) dst[i] = pk_bf16(rat[2 * i], rat[2 * i + 1]);
+}
+hipError_t launch_pack_ratings(const float* rat, uint32_t* dst, int64_t n_pairs, hipStream_t s) {
+    if (n_pairs <= 0) return hipSuccess;
+    als_pack_ratings<<<(unsigned)((n_pairs + 255) / 256), 256, 0, s>>>(rat, dst, n_pairs);
+    return hipGetLastError();
+}
 hipError_t launch_presplit(const float* src, void* dst, int64_t n_rows, hipStream_t s) {
     const int64_t pieces = n_rows * 16;
     if (pieces <= 0) return hipSuccess;
