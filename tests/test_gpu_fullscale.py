@@ -120,7 +120,7 @@ def test_powerlaw_shard_sampled_rows(cfk, oracle_mod):
           f"user {worst_u:.2e}")
 
 
-def _k128_worker(rank, world, port, out_dir):
+def _sharded_worker(rank, world, port, out_dir, k):
     import sys
     from conftest import ROOT
     sys.path.insert(0, ROOT)
@@ -130,7 +130,7 @@ def _k128_worker(rank, world, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ds = cfk.Dataset.synthetic_netflix(n_users=3000, n_movies=400, nnz=90_000, seed=11, nthreads=8)
-    app = cfk.ALSApp(world, 128, LAM, 3, precision="f32", seed=9, device=0, rank=rank, world_size=world,
+    app = cfk.ALSApp(world, k, LAM, 3, precision="f32", seed=9, device=0, rank=rank, world_size=world,
                      overlap_chunks=3)
     app.setup(ds)
     app.run()
@@ -139,21 +139,23 @@ def _k128_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_sharded_k128_two_ranks_chunked(tmp_path, oracle_mod, cfk):
+@pytest.mark.parametrize("k", [64, 128])
+def test_sharded_two_ranks_chunked(tmp_path, oracle_mod, cfk, k):
     """BASELINE configs[3] path at test size: k = 128 (KP = 128 MFMA variants) sharded over 2 ranks (both on
     cuda:0, gloo carrying the all-gathers) with the user half in 3 overlapped chunks; MSE delta <= 1e-3 and
-    factors within 1e-3 norm-relative of the fp64 oracle."""
+    factors within 1e-3 norm-relative of the fp64 oracle. At k = 64 the same run covers the chunked pre-split user
+    half (3 waves per SIMD, packed bf16 rating pairs; chunk 0 prepares the pre-split table for the later chunks)."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    mp.spawn(_k128_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_sharded_worker, args=(2, port, str(tmp_path), k), nprocs=2, join=True)
     ds = cfk.Dataset.synthetic_netflix(n_users=3000, n_movies=400, nnz=90_000, seed=11, nthreads=8)
     m, u, r = ds.ratings()
     b = oracle_mod.build_blocks(m, u, r)
-    Uo, Mo = oracle_mod.run_als(b, 128, LAM, 3, seed=9, precision="f64")
+    Uo, Mo = oracle_mod.run_als(b, k, LAM, 3, seed=9, precision="f64")
     mse_o = oracle_mod.mse(b, Uo, Mo)
     for rank in range(2):
         res = np.load(os.path.join(tmp_path, f"rank{rank}.npz"))
