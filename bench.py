@@ -231,6 +231,12 @@ def main():
                 "traffic": (tr or {}).get("per_side", {}).get(side),
                 "alg_gram_tflops": gram_f / t_s / 1e12, "alg_solve_tflop_per_launch": solve_f / 1e12,
                 "short_rows_entry_space": dual,
+                # what bounds the launch (PMC passes in profiles/): the HBM fraction above is in
+                # algorithmic bytes; the pre-split half reads an L2-resident table and is issue-bound instead
+                "limit": ("issue: 64 MFMA + ~80 VALU per 32-entry block on one SIMD issue port, 3 waves/SIMD; "
+                          "opposite table L2-resident (pre-split)") if path["presplit"] else
+                         ("Infinity-Cache / fabric gather of the opposite factor rows" if kp <= 64 else
+                          "HBM gather of the opposite factor rows + one-wave-per-SIMD solve"),
                 "mfma_bf16": {"per_32_entry_block": mfma_per_block(kp, path["presplit"]),
                               "executed_tflops": mf / t_s / 1e12, "peak": BF16_MFMA_PEAK_TFS,
                               "frac": mf / t_s / 1e12 / BF16_MFMA_PEAK_TFS},
