@@ -3,7 +3,7 @@
 (with the user half run in between, which reuses the shared partial-slot workspace) must give identical
 factors. Variants are env settings applied at engine creation.
 
-  [DET_K=128] [DET_REPS=3] python tools/determinism.py [VAR=VAL[,VAR=VAL]] ...
+  [DET_K=128] [DET_REPS=3] [DET_USER_REPS=40] python tools/determinism.py [VAR=VAL[,VAR=VAL]] ...
 """
 import os
 import sys
@@ -64,6 +64,19 @@ def main():
             print(f"{v}: movie rep0 vs rep{r}: {len(rows)} differing rows {rows[:12].tolist()} rel {rel}; "
                   f"degrees {deg[rows][:12].tolist()}; "
                   f"stats {eng.block_stats(0)}", flush=True)
+        ureps = int(os.environ.get("DET_USER_REPS", "0"))
+        if ureps:
+            # the user half repeated on the same movie factors (the pre-split, 3-wave path at k = 64): every
+            # repetition must reproduce the first bitwise
+            U_first, bad = None, []
+            for rep in range(ureps):
+                eng.solve_half(1, 0.05)
+                U = eng.read_factors(1)
+                if U_first is None:
+                    U_first = U
+                else:
+                    bad.append(int(np.count_nonzero(np.any(U != U_first, axis=1))))
+            print(f"{v}: user half x{ureps}: differing rows per repetition {bad}; total {sum(bad)}", flush=True)
         eng.close()
 
 
