@@ -11,10 +11,16 @@ generator). Inputs are resident in HBM before the timed region. 
 (strong scaling): users and movies are sharded by id % N, one process per GPU.
 
 Prints ONE JSON line (rank 0). `roofline` describes the dominant kernel launch (the slower of the two halves'
-fused gather/Gram/solve launches; both are under roofline.per_launch) with the algorithmic bytes of SURVEY.md
-§8d, timed with HIP events on the stream the kernel is launched on; `cpu_baseline` times the oracle's
-Java-float restatement of the reference hot path (the "port") on a bounded sample of the same workload, with
-the reference's 4 stream threads (BaseKafkaApp.java:51) and with the box's CPU share, rank 0 at N = 1 only.
+fused gather/Gram/solve launches; both are under roofline.per_launch), timed with HIP events on the stream the
+kernel is launched on. Its `bound` is the launch's real limiter, from the rocprofv3 counters of the same build
+(profiles/counters_k<k>.json, written by tools/prof_summary.py from a profiles/r03*/ pass): the pre-split user
+half and every KP = 128 launch are bound by the MFMA pipe (achieved = the split-bf16 Gram's MFMA flops as issued,
+against the dense bf16 peak), the on-the-fly-split movie half at k = 64 by the fabric gather of the opposite rows
+(counter bytes / time against the Infinity-Cache gather ceiling). The SURVEY.md §8d algorithmic-byte fraction
+stays as a secondary field (cache-served gathers included, so it can exceed 1). `cpu_baseline` times the
+oracle's Java-float restatement of the reference hot path (the "port", one C call per sampled half) on a bounded
+sample of the same workload with the reference's 4 stream threads (BaseKafkaApp.java:51), the box's CPU share
+and all `nproc` CPUs, rank 0 at N = 1 only.
 """
 from __future__ import annotations
 
@@ -30,6 +36,9 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFS = 157.3        # f32 vector = f32 MFMA dense peak
 BF16_MFMA_PEAK_TFS = 2500.0  # dense bf16 MFMA peak (no sparsity)
+# MI355X_MICROARCH.md "Indexed rows: gather into LDS": uniformly random rows of a 151 MB table (the 123 MB k = 64
+# user table the movie half gathers sits between its 38 MB and 151 MB rows) are served at 7.4-7.9 TB/s chip-wide
+IC_GATHER_CEILING_GBS = 7900.0
 MFMA_BF16_FLOP = 16 * 16 * 32 * 2   # one v_mfma_f32_16x16x32_bf16
 
 
@@ -110,21 +119,25 @@ def cpu_baseline(ds, k, lam, seconds, thread_counts):
         runs.append({"threads": threads, "value": r / t, "ratings_per_half": r, "seconds": t})
     main = runs[0]
     return {"value": main["value"], "unit": "ratings/s", "cores": main["threads"], "kind": "port",
-            "sample": f"oracle f32 (Java-float EJML-order restatement of MFeatureCalculator/UFeatureCalculator) on "
-                      f"random rows of both halves, {main['ratings_per_half']} ratings per half "
+            "sample": f"oracle f32 (Java-float EJML-order restatement of MFeatureCalculator/UFeatureCalculator, "
+                      f"oracle/als_oracle.c, ONE C call per half over the sampled rows) on uniformly random rows of "
+                      f"both halves, {main['ratings_per_half']} ratings per half "
                       f"({main['ratings_per_half'] / ds.nnz * 100:.2f}% of a half), {main['seconds']:.1f} s, "
-                      f"{main['threads']} threads = the reference's NUM_STREAM_THREADS (BaseKafkaApp.java:51)",
+                      f"{main['threads']} threads = the reference's NUM_STREAM_THREADS (BaseKafkaApp.java:51). "
+                      f"Representative: a row costs deg k^2 + k^3 / 3 flops, and rows drawn uniformly carry the "
+                      f"half's own degree mix, so ratings / s over the sample estimates the full half's rate",
             "runs": runs, "cpu_model": cpu_model(), "nproc": os.cpu_count(),
             "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
 
 
-def load_traffic(k, nnz):
-    path = os.path.join(ROOT, "profiles", "traffic.json" if k == 64 else f"traffic_k{k}.json")
+def load_counters(k, nnz):
+    """Per-launch rocprofv3 counters of this build at (k, nnz): profiles/counters_k<k>.json (tools/prof_summary.py)."""
+    path = os.path.join(ROOT, "profiles", f"counters_k{k}.json")
     try:
-        tr = json.load(open(path))
+        c = json.load(open(path))
     except (OSError, ValueError):
         return None
-    return tr if tr.get("k") == k and tr.get("nnz") == nnz else None
+    return c if c.get("k") == k and c.get("nnz") == nnz else None
 
 
 def main():
@@ -141,6 +154,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=7.0, help="CPU baseline seconds per thread count")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--overlap-chunks", type=int, default=4, help="user-half chunks per all-gather overlap (N > 1)")
+    ap.add_argument("--exchange", choices=("torch", "native"), default="torch",
+                    help="N > 1: all-gathers through torch.distributed (RCCL) or through the engine's own RCCL "
+                         "communicator behind the C ABI (als_comm_init / als_allgather_shard, the path a JNI caller "
+                         "binds)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N > 1 ranks all on cuda:0 over gloo: rehearses the multi-rank driver on a one-GPU box "
                          "(RCCL needs one GPU per rank); not a performance configuration")
@@ -172,8 +189,10 @@ def main():
     t_setup = time.perf_counter()
     ds = cfk.Dataset.synthetic_netflix(args.users, args.movies, args.nnz, args.seed, nthreads=min(16, os.cpu_count()))
     nm, nu, nnz = ds.counts()
+    exchange = args.exchange if world > 1 and not args.rehearse_one_gpu else "torch"
     app = cfk.ALSApp(world, args.k, args.lam, args.steps, precision="f32", seed=42, device=local, rank=rank,
-                     world_size=world, overlap_chunks=args.overlap_chunks).setup(ds, check_duplicates=False)
+                     world_size=world, overlap_chunks=args.overlap_chunks,
+                     exchange=exchange).setup(ds, check_duplicates=False)
     t_setup = time.perf_counter() - t_setup
 
     for _ in range(args.warmup):
@@ -207,7 +226,7 @@ def main():
 
     if rank == 0:
         info = {"movie": app.info[0], "user": app.info[1]}
-        tr = load_traffic(args.k, nnz) if world == 1 else None
+        ctr = load_counters(args.k, nnz) if world == 1 else None
         kp = eng.kp
         per = {}
         for si, side in enumerate(("movie", "user")):
@@ -222,44 +241,64 @@ def main():
             t_s = g_ms[side] / 1000.0
             mf = ((main_blocks * mfma_per_block(kp, path["presplit"]) + dual_mfma) * MFMA_BF16_FLOP
                   if path["gram_path"] == "mfma_split" else 0)
-            achieved = b / t_s / 1e9
-            per[side] = {
+            c = (ctr or {}).get("per_side", {}).get(side, {})
+            gather_bound = kp <= 64 and not path["presplit"]
+            d = {
                 "kernel": f"als_solve_mfma<{kp},{1 if kp == 128 else (3 if path['presplit'] else 2)},split,"
                           f"{'presplit' if path['presplit'] else 'on-the-fly split'}> + als_solve_dual (short rows)",
                 "avg_launch_ms": g_ms[side], "reduce_launch_ms": r_ms[side],
-                "algorithmic_bytes": b, "achieved": achieved, "frac": achieved / HBM_PEAK_GBS,
-                "traffic": (tr or {}).get("per_side", {}).get(side),
-                "alg_gram_tflops": gram_f / t_s / 1e12, "alg_solve_tflop_per_launch": solve_f / 1e12,
-                "short_rows_entry_space": dual,
-                # what bounds the launch (PMC passes in profiles/): the HBM fraction above is in
-                # algorithmic bytes; the pre-split half reads an L2-resident table and is issue-bound instead
-                "limit": ("issue: 64 MFMA + ~80 VALU per 32-entry block on one SIMD issue port, 3 waves/SIMD; "
-                          "opposite table L2-resident (pre-split)") if path["presplit"] else
-                         ("Infinity-Cache / fabric gather of the opposite factor rows" if kp <= 64 else
-                          "HBM gather of the opposite factor rows + one-wave-per-SIMD solve"),
                 "mfma_bf16": {"per_32_entry_block": mfma_per_block(kp, path["presplit"]),
-                              "executed_tflops": mf / t_s / 1e12, "peak": BF16_MFMA_PEAK_TFS,
+                              "flop_per_launch": mf, "executed_tflops": mf / t_s / 1e12, "peak": BF16_MFMA_PEAK_TFS,
                               "frac": mf / t_s / 1e12 / BF16_MFMA_PEAK_TFS},
+                "algorithmic_bytes": {"bytes": b, "achieved_gbs": b / t_s / 1e9, "frac_of_hbm": b / t_s / 1e9 / HBM_PEAK_GBS,
+                                      "note": "SURVEY.md §8d algorithmic bytes / launch time; cache-served gathers "
+                                              "included, so it can exceed 1: not a bound"},
+                "algorithmic_fp32": {"gram_flop": gram_f, "solve_flop": solve_f,
+                                     "tflops": (gram_f + solve_f) / t_s / 1e12, "fp32_peak": FP32_PEAK_TFS},
+                "short_rows_entry_space": dual,
             }
+            if c:
+                d["counters"] = c
+                d["traffic"] = c.get("hbm_bytes")
+            if gather_bound:
+                # the fabric gather of the opposite factor rows (L2 misses served by the Infinity Cache / HBM)
+                fab = c.get("hbm_bytes")
+                d.update(bound="gather", unit="GB/s", peak=IC_GATHER_CEILING_GBS,
+                         achieved=(fab / t_s / 1e9) if fab else None,
+                         limit="fabric gather of the opposite factor rows: PMC FETCH x2 + WRITE bytes / launch time "
+                               "against the Infinity-Cache random-row gather ceiling (MI355X_MICROARCH.md)")
+            else:
+                d.update(bound="mfma", unit="TFLOP/s", peak=BF16_MFMA_PEAK_TFS, achieved=mf / t_s / 1e12,
+                         limit="MFMA pipe: the split-bf16 Gram's v_mfma_f32_16x16x32_bf16 flops as issued against "
+                               "the dense bf16 peak; counters.mfma_busy_frac = pipe-busy share of the launch")
+            d["frac"] = d["achieved"] / d["peak"] if d.get("achieved") else None
+            per[side] = d
         dom = max(per, key=lambda s: per[s]["avg_launch_ms"])
         d = per[dom]
         roofline = {
-            "bound": "hbm", "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": d["frac"],
-            "traffic": d["traffic"], "kernel": d["kernel"] + f" ({dom} half, the dominant launch)",
-            "algorithmic_bytes_per_launch": d["algorithmic_bytes"], "avg_launch_ms": d["avg_launch_ms"],
-            "both_halves": {"achieved": (per["movie"]["algorithmic_bytes"] + per["user"]["algorithmic_bytes"])
-                            / ((g_ms["movie"] + g_ms["user"]) / 1000.0) / 1e9},
+            "bound": d["bound"] if d["bound"] == "mfma" else "hbm", "achieved": d["achieved"], "peak": d["peak"],
+            "unit": d["unit"], "frac": d["frac"], "traffic": d.get("traffic"),
+            "kernel": d["kernel"] + f" ({dom} half, the dominant launch)", "limit": d["limit"],
+            "avg_launch_ms": d["avg_launch_ms"], "counters": d.get("counters"),
+            "algorithmic_bytes_frac": d["algorithmic_bytes"]["frac_of_hbm"],
+            "both_halves_algorithmic_gbs": (per["movie"]["algorithmic_bytes"]["bytes"] +
+                                            per["user"]["algorithmic_bytes"]["bytes"])
+                                           / ((g_ms["movie"] + g_ms["user"]) / 1000.0) / 1e9,
             "per_launch": per,
-            "note": "achieved = SURVEY.md §8d algorithmic bytes / HIP-event launch time; traffic = PMC FETCH_SIZE x2 + "
-                    "WRITE_SIZE per launch (profiles/traffic.json); mfma_bf16 = executed v_mfma_f32_16x16x32_bf16 "
-                    "flops of the split Gram (each fp32 product = 3-term bf16 split: 6 partial products per "
-                    "off-diagonal tile) against the dense bf16 peak",
+            "counters_source": (ctr or {}).get("source"),
+            "note": "achieved/frac: the dominant launch against its binding ceiling (bound); traffic = PMC FETCH_SIZE "
+                    "x2 + WRITE_SIZE per launch; counters = rocprofv3 SQ passes of this build (whole launch, Gram only, "
+                    "and their difference = the solve phase)",
         }
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-            share = min(share, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
-            cpu = cpu_baseline(ds, args.k, args.lam, args.cpu_seconds, [4] + ([share] if share != 4 else []))
+            ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+            share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or ncpu   # the box's CPU share (16 on one GPU)
+            counts = []
+            for t in (4, min(share, ncpu), ncpu):                   # reference's stream threads, share, nproc
+                if t not in counts:
+                    counts.append(t)
+            cpu = cpu_baseline(ds, args.k, args.lam, args.cpu_seconds, counts)
         value = nnz * K / elapsed
         line = {
             "metric": "ALS ratings/sec per full iteration, k=64 Netflix-shape, 1/2/4/8 MI355X",
@@ -269,7 +308,9 @@ def main():
             "config": {"workload": f"netflix-shape synthetic {nu} users x {nm} movies x {nnz} ratings, k={args.k}, "
                                    f"lambda={args.lam}, one step = one full ALS iteration",
                        "n_users": nu, "n_movies": nm, "nnz": nnz, "k": args.k, "lambda": args.lam,
-                       "seed": args.seed, "partitions": world, "parallelism": f"id%{world} shards + RCCL all-gather"},
+                       "seed": args.seed, "partitions": world, "parallelism": f"id%{world} shards + RCCL all-gather",
+                       "exchange": exchange if world > 1 else None,
+                       "overlap_chunks": args.overlap_chunks if world > 1 else None},
             "solves_per_s": (nm + nu) * K / elapsed,
             "mse_after": mse,
             "setup_s": t_setup,

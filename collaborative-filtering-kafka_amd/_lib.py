@@ -76,7 +76,8 @@ SIGNATURES = [
     ("als_comm_init", _i, [_vp, _i, _i, _vp]),
     ("als_comm_init_group", _i, [_ppv, _i]),
     ("als_comm_info", _i, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
-    ("als_allgather_shard", _i, [_vp, _i, _i64, _i64, _i64]),
+    ("als_allgather_shard", _i, [_vp, _i, _i64, _i64]),
+    ("als_set_row_layout", _i, [_vp, _i, _i64, _i64]),
     ("als_comm_group_start", _i, []),
     ("als_comm_group_end", _i, []),
     ("als_comm_wait", _i, [_vp]),
@@ -100,6 +101,8 @@ SIGNATURES = [
     ("als_dataset_ratings", _i, [_vp, _pi32, _pi32, _pi16]),
     ("als_dataset_count_duplicates", _i, [_vp, _pi64]),
     ("als_dataset_shard_info", _i, [_vp, _i, _i, _i, _pi64, _pi64, _pi64, _pi64, _pi64]),
+    ("als_dataset_set_slot_chunks", _i, [_vp, _i, _i]),
+    ("als_dataset_slot_layout", _i, [_vp, _i, _i, _pi64, ctypes.POINTER(ctypes.c_int)]),
     ("als_dataset_shard_block", _i, [_vp, _i, _i, _i64, _pi64, _pi32, _pi16, _pi64]),
     ("als_dataset_shard_coo", _i, [_vp, _i, _i, _i64, _pi32, _pi32, _pi16]),
     ("als_dataset_slots", _i, [_vp, _i, _i, _pi64]),

@@ -72,6 +72,11 @@ class ALSApp:
             raise ValueError("duplicate (user, movie) pairs: the reference never completes such an entity "
                              "(MFeatureCalculator.java:65)")
         self.ds = ds
+        # user half on > 1 GPU in `overlap_chunks` row ranges: chunk-major user slots (include/als_host.h "Slot
+        # layout"), so each range's exchange is one contiguous all-gather
+        n_chunks = self.overlap_chunks if self.world > 1 else 1
+        ds.set_slot_chunks(SIDE_USER, n_chunks)
+        ds.set_slot_chunks(SIDE_MOVIE, 1)
         if engine_factory is None:
             torch.cuda.set_device(self.device)
             eng = ALSEngine(self.NUM_FEATURES, self.precision, self.device)
@@ -90,17 +95,17 @@ class ALSApp:
                 blk = ds.shard_block(side, self.world, self.rank)
                 eng.alloc_factors(side, blk["n_slots"])
                 eng.set_block(side, blk["row_ptr"], blk["col"], blk["ratings"], blk["row_offset"], opp["n_slots"])
-            self.info[side] = {k: blk[k] for k in ("n_rows", "row_offset", "nnz", "slots_per_shard", "n_slots")}
-        if self.world > 1 and self.overlap_chunks > 1:
-            S = self.info[SIDE_USER]["slots_per_shard"]
-            n = self.info[SIDE_USER]["n_rows"]
-            Sc = -(-S // self.overlap_chunks)
-            starts = [min(c * Sc, S) for c in range(self.overlap_chunks + 1)]
-            # chunk c = slots [starts[c], starts[c+1]) of every shard; this rank solves its rows there
-            self.chunk_slots = [(starts[c], starts[c + 1]) for c in range(self.overlap_chunks)
-                                if starts[c + 1] > starts[c]]
-            bounds = [0] + [min(hi, n) for _, hi in self.chunk_slots]
-            eng.set_chunks(SIDE_USER, bounds)
+            sc, nc = ds.slot_layout(side, self.world)
+            blk["slots_per_chunk"], blk["n_chunks"] = sc, nc
+            if nc > 1:
+                eng.set_row_layout(side, sc, self.world * sc)
+            self.info[side] = {k: blk[k] for k in ("n_rows", "row_offset", "nnz", "slots_per_shard", "n_slots",
+                                                   "slots_per_chunk", "n_chunks")}
+        if n_chunks > 1:
+            sc, n = self.info[SIDE_USER]["slots_per_chunk"], self.info[SIDE_USER]["n_rows"]
+            # chunk c = this rank's local rows [c Sc, (c+1) Sc) = factor rows [c G Sc + rank Sc, + Sc)
+            self.chunk_slots = list(range(n_chunks))
+            eng.set_chunks(SIDE_USER, [min(c * sc, n) for c in range(n_chunks)] + [n])
         u0 = ds.init_user_factors(self.NUM_FEATURES, self.seed, self.world)
         eng.write_factors(SIDE_USER, u0)
         if self.exchange == "native" and self.world > 1:
@@ -121,48 +126,47 @@ class ALSApp:
             self._ordered = dist.get_backend(self.group) == "nccl"
         return self._ordered
 
-    def _allgather(self, side: int):
+    def _allgather(self, side: int, chunk: int = 0):
+        """Exchange chunk `chunk` of `side` (the whole shard when the side is unchunked): one all-gather of the G
+        ranks' Sc-row pieces, which are contiguous in the chunk-major slot layout."""
         if self.world == 1:
             return
+        sc = self.info[side]["slots_per_chunk"]
         if self.exchange == "native":
-            self.engine.allgather_shard(side, self.info[side]["slots_per_shard"])
+            self.engine.allgather_shard(side, sc, chunk)
             return
         import torch.distributed as dist
         if not self._stream_ordered():
             self.engine.synchronize()
-        S = self.info[side]["slots_per_shard"]
-        full = self.engine.factors[side]            # [G*S + 1, kp]: last row = sentinel, not exchanged
-        dist.all_gather_into_tensor(full[:self.world * S], full[self.rank * S:(self.rank + 1) * S], group=self.group)
+        full = self.engine.factors[side]            # [n_slots + 1, kp]: last row = sentinel, not exchanged
+        base = chunk * self.world * sc
+        return dist.all_gather_into_tensor(full[base:base + self.world * sc],
+                                           full[base + self.rank * sc:base + (self.rank + 1) * sc],
+                                           group=self.group, async_op=True)
 
     def movie_half(self):
         """MFeatureCalculator-i over this rank's movies + all-gather (movie-features-i topic)."""
         self.engine.solve_half(SIDE_MOVIE, self.ALS_LAMBDA)
-        self._allgather(SIDE_MOVIE)
+        w = self._allgather(SIDE_MOVIE)
+        if w is not None:
+            w.wait()
 
     def user_half(self):
         """UFeatureCalculator-i over this rank's users + all-gather (user-features-(i+1) topic)."""
         if self.chunk_slots is None:
             self.engine.solve_half(SIDE_USER, self.ALS_LAMBDA)
-            self._allgather(SIDE_USER)
+            w = self._allgather(SIDE_USER)
+            if w is not None:
+                w.wait()
             return
-        # chunk c's all-gather (RCCL stream, ordered after chunk c's solve) overlaps chunk c+1's solve
-        S = self.info[SIDE_USER]["slots_per_shard"]
-        if self.exchange == "native":
-            for c, (lo, hi) in enumerate(self.chunk_slots):
-                self.engine.solve_half_chunk(SIDE_USER, self.ALS_LAMBDA, c)
-                self.engine.allgather_shard(SIDE_USER, S, lo, hi)
-            return
-        import torch.distributed as dist
-        U = self.engine.factors[SIDE_USER]
+        # chunk c's all-gather (RCCL, ordered after chunk c's solve on the stream) overlaps chunk c+1's solve
         works = []
-        for c, (lo, hi) in enumerate(self.chunk_slots):
+        for c in self.chunk_slots:
             self.engine.solve_half_chunk(SIDE_USER, self.ALS_LAMBDA, c)
-            if not self._stream_ordered():
-                self.engine.synchronize()
-            outs = [U[g * S + lo:g * S + hi] for g in range(self.world)]
-            works.append(dist.all_gather(outs, outs[self.rank], group=self.group, async_op=True))
+            works.append(self._allgather(SIDE_USER, c))
         for w in works:
-            w.wait()
+            if w is not None:
+                w.wait()
 
     def iteration(self):
         self.movie_half()

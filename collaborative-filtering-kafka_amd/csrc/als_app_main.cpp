@@ -173,7 +173,7 @@ int main(int argc, char** argv) {
             if (als_solve_half(eng[g], side, lambda) != ALS_OK) return false;
         if (als_comm_group_start() != ALS_OK) return false;
         for (int g = 0; g < G; ++g)
-            if (als_allgather_shard(eng[g], side, S[side], 0, S[side]) != ALS_OK) return false;
+            if (als_allgather_shard(eng[g], side, S[side], 0) != ALS_OK) return false;   // one chunk
         return als_comm_group_end() == ALS_OK;
     };
     struct timeval t0, t1;

@@ -49,6 +49,7 @@ struct als_dataset {
     // derived
     std::vector<int64_t> ids[2];      // ascending raw ids per side (0 = movie, 1 = user)
     std::vector<int32_t> dense[2];    // per rating: dense (ascending-id rank) index of its movie / user
+    int chunks[2] = {1, 1};           // chunk-major slot layout per side (als_dataset_set_slot_chunks)
 };
 
 namespace {
@@ -78,28 +79,41 @@ void finalize(als_dataset* ds) {
     }
 }
 
-// Shard geometry of one side under G shards.
+// Shard geometry of one side under G shards and C chunks (als_host.h "Slot layout"): entity i of shard
+// sh = id % G with rank r among that shard's ids (ascending) sits at slot (r / Sc) * (G * Sc) + sh * Sc + r % Sc,
+// Sc = ceil(S / C), S = the largest shard. C = 1: slot = sh * S + r (shard-major).
 struct ShardMap {
-    int G = 1;
-    int64_t S = 0;                        // slots per shard
+    int G = 1, C = 1;
+    int64_t S = 0;                        // rows of the largest shard
+    int64_t Sc = 0;                       // slots per shard and chunk
     std::vector<int64_t> slot;            // per dense entity
+    std::vector<int32_t> shard;           // per dense entity
+    std::vector<int64_t> local;           // per dense entity: its row in its shard's block (= rank)
     std::vector<int64_t> count;           // entities per shard
+    int64_t n_slots() const { return (int64_t)C * G * Sc; }
 };
 
 ShardMap shard_map(const als_dataset* ds, int side, int G) {
     ShardMap m;
     m.G = G;
+    m.C = ds->chunks[side];
     const auto& ids = ds->ids[side];
     m.count.assign(G, 0);
     m.slot.resize(ids.size());
-    std::vector<int64_t> rank(ids.size());
+    m.shard.resize(ids.size());
+    m.local.resize(ids.size());
     for (size_t i = 0; i < ids.size(); ++i) {
         const int sh = (int)(ids[i] % G);   // PureModStreamPartitioner.java:10
-        rank[i] = m.count[sh]++;
+        m.shard[i] = sh;
+        m.local[i] = m.count[sh]++;
     }
     m.S = 0;
     for (int64_t c : m.count) m.S = std::max(m.S, c);
-    for (size_t i = 0; i < ids.size(); ++i) m.slot[i] = (ids[i] % G) * m.S + rank[i];
+    m.Sc = (m.S + m.C - 1) / m.C;
+    for (size_t i = 0; i < ids.size(); ++i) {
+        const int64_t r = m.local[i];
+        m.slot[i] = (r / m.Sc) * ((int64_t)G * m.Sc) + (int64_t)m.shard[i] * m.Sc + r % m.Sc;
+    }
     return m;
 }
 
@@ -554,10 +568,24 @@ int als_dataset_shard_info(const als_dataset* ds, int side, int n_shards, int sh
     const auto& raw = side == 0 ? ds->movie : ds->user;
     for (int32_t v : raw) z += (v % n_shards) == shard;
     if (n_rows) *n_rows = m.count[shard];
-    if (row_offset) *row_offset = shard * m.S;
+    if (row_offset) *row_offset = shard * m.Sc;
     if (nnz) *nnz = z;
-    if (slots_per_shard) *slots_per_shard = m.S;
-    if (n_slots) *n_slots = m.S * n_shards;
+    if (slots_per_shard) *slots_per_shard = m.Sc * m.C;
+    if (n_slots) *n_slots = m.n_slots();
+    return ALS_OK;
+}
+
+int als_dataset_set_slot_chunks(als_dataset* ds, int side, int n_chunks) {
+    if (!ds || (side != 0 && side != 1) || n_chunks < 1) return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));
+    ds->chunks[side] = n_chunks;
+    return ALS_OK;
+}
+
+int als_dataset_slot_layout(const als_dataset* ds, int side, int n_shards, int64_t* slots_per_chunk, int* n_chunks) {
+    if (!ds || (side != 0 && side != 1) || n_shards < 1) return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));
+    const ShardMap m = shard_map(ds, side, n_shards);
+    if (slots_per_chunk) *slots_per_chunk = m.Sc;
+    if (n_chunks) *n_chunks = m.C;
     return ALS_OK;
 }
 
@@ -569,33 +597,27 @@ int als_dataset_shard_block(const als_dataset* ds, int side, int n_shards, int64
     const ShardMap ms = shard_map(ds, side, n_shards);
     const ShardMap mo = shard_map(ds, opp, n_shards);
     const int64_t nr = ms.count[shard];
-    const int64_t base = shard * ms.S;
     const auto& dn = ds->dense[side];
     const auto& dop = ds->dense[opp];
     const int64_t n = (int64_t)dn.size();
     // stable counting sort of arrival order by local row: in-block order = arrival order
     std::fill(row_ptr, row_ptr + nr + 1, 0);
-    for (int64_t t = 0; t < n; ++t) {
-        const int64_t s = ms.slot[dn[t]];
-        if (s >= base && s < base + nr) ++row_ptr[s - base + 1];
-    }
+    for (int64_t t = 0; t < n; ++t)
+        if (ms.shard[dn[t]] == shard) ++row_ptr[ms.local[dn[t]] + 1];
     for (int64_t i = 0; i < nr; ++i) row_ptr[i + 1] += row_ptr[i];
     if (col_idx || ratings) {
         std::vector<int64_t> pos(row_ptr, row_ptr + nr);
         for (int64_t t = 0; t < n; ++t) {
-            const int64_t s = ms.slot[dn[t]];
-            if (s < base || s >= base + nr) continue;
-            const int64_t p = pos[s - base]++;
+            if (ms.shard[dn[t]] != shard) continue;
+            const int64_t p = pos[ms.local[dn[t]]]++;
             if (col_idx) col_idx[p] = (int32_t)mo.slot[dop[t]];
             if (ratings) ratings[p] = ds->rating[t];
         }
     }
     if (row_ids) {
         const auto& ids = ds->ids[side];
-        for (size_t i = 0; i < ids.size(); ++i) {
-            const int64_t s = ms.slot[i];
-            if (s >= base && s < base + nr) row_ids[s - base] = ids[i];
-        }
+        for (size_t i = 0; i < ids.size(); ++i)
+            if (ms.shard[i] == shard) row_ids[ms.local[i]] = ids[i];
     }
     return ALS_OK;
 }
@@ -607,16 +629,13 @@ int als_dataset_shard_coo(const als_dataset* ds, int side, int n_shards, int64_t
     const int opp = 1 - side;
     const ShardMap ms = shard_map(ds, side, n_shards);
     const ShardMap mo = shard_map(ds, opp, n_shards);
-    const int64_t nr = ms.count[shard];
-    const int64_t base = shard * ms.S;
     const auto& dn = ds->dense[side];
     const auto& dop = ds->dense[opp];
     const int64_t n = (int64_t)dn.size();
     int64_t p = 0;
     for (int64_t t = 0; t < n; ++t) {   // arrival order: the order the block builder sees the ratings
-        const int64_t s = ms.slot[dn[t]];
-        if (s < base || s >= base + nr) continue;
-        rows[p] = (int32_t)(s - base);
+        if (ms.shard[dn[t]] != shard) continue;
+        rows[p] = (int32_t)ms.local[dn[t]];
         cols[p] = (int32_t)mo.slot[dop[t]];
         ratings[p] = ds->rating[t];
         ++p;
@@ -637,7 +656,7 @@ int als_dataset_init_user_factors(const als_dataset* ds, int num_features, uint6
     if (!ds || num_features < 1 || n_shards < 1 || !out || ld < num_features)
         return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad arguments"));
     const ShardMap m = shard_map(ds, 1, n_shards);
-    if (n_out_rows < m.S * n_shards) return report(fail(ALS_ERR_INVALID_ARGUMENT, "output has too few rows"));
+    if (n_out_rows < m.n_slots()) return report(fail(ALS_ERR_INVALID_ARGUMENT, "output has too few rows"));
     std::fill(out, out + n_out_rows * ld, 0.f);
     const int64_t nu = (int64_t)ds->ids[1].size();
     std::vector<int64_t> sum(nu, 0), cnt(nu, 0);

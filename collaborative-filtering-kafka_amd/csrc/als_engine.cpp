@@ -64,6 +64,13 @@ struct Block {
     Task* d_sq_tasks = nullptr;     // every FULL + PARTIAL task incl. the short rows (als_sq_error)
     int32_t n_sq = 0;
     bool presplit = false;          // gather a pre-split (bf16 h/m/l) copy of the opposite table
+    // chunk-major slot layout (als_set_row_layout): local row i -> factor row row_offset + (i / rows_per_chunk) *
+    // chunk_stride + i % rows_per_chunk; rows_per_chunk = 0: row_offset + i
+    int64_t rows_per_chunk = 0, chunk_stride = 0;
+    int64_t factor_row(int64_t i) const {
+        return rows_per_chunk > 0 ? row_offset + (i / rows_per_chunk) * chunk_stride + i % rows_per_chunk
+                                  : row_offset + i;
+    }
 };
 
 struct TimingRec {
@@ -100,9 +107,7 @@ struct als_engine {
     size_t stage_bytes = 0;
     uint32_t* d_integrity = nullptr;   // cfk::INTEGRITY_WORDS: partial slots that failed their check
     uint32_t gen = 0;               // launch generation of the next PARTIAL/REDUCE pair
-    int min_waves = 0;              // ALS_MFMA_WAVES override of the per-block occupancy choice (0 = auto)
-    int split_waves = 2;            // ALS_SPLIT_WAVES: waves per SIMD of the on-the-fly split-bf16 variant
-    int32_t debug_flags = 0;        // ALS_DEBUG_SKIP_SOLVE=1 -> cfk::SOLVE_FLAG_SKIP_SOLVE (tools/kbench.py only)
+    int32_t debug_flags = 0;        // debug build only (CFK_DEBUG_KNOBS): ALS_DEBUG_SKIP_SOLVE / _REFINE
     uint32_t debug_gen_skew = 0;    // ALS_DEBUG_REDUCE_GEN_SKEW=n: REDUCE decodes with generation + n (tests the
                                     // integrity check: every slot then reads as written by another launch)
     // ALS_REFINE_MIN_PIVOT (cfk::SolveArgs): 0.45 keeps the worst per-row error ratio to the reference's own fp32
@@ -246,16 +251,18 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
     e->kp = kp;
     e->precision = precision;
     e->path = path;
-    if (const char* env = getenv("ALS_MFMA_WAVES")) e->min_waves = std::max(0, atoi(env));
-    if (const char* env = getenv("ALS_SPLIT_WAVES")) e->split_waves = std::max(2, atoi(env));
+#ifdef CFK_DEBUG_KNOBS
+    // work-dropping diagnostics: compiled only into the tools' debug build (Makefile target `debug`), never into
+    // the product library
     if (const char* env = getenv("ALS_DEBUG_SKIP_SOLVE"))
         if (env[0] == '1') e->debug_flags |= cfk::SOLVE_FLAG_SKIP_SOLVE;
+    if (const char* env = getenv("ALS_DEBUG_SKIP_REFINE"))
+        if (env[0] == '1') e->debug_flags |= cfk::SOLVE_FLAG_SKIP_REFINE;
+#endif
     if (const char* env = getenv("ALS_DEBUG_REDUCE_GEN_SKEW")) e->debug_gen_skew = (uint32_t)atoi(env);
     if (const char* env = getenv("ALS_DEBUG_FIXED_GEN")) e->debug_fixed_gen = env[0] == '1';
     if (const char* env = getenv("ALS_REFINE_MIN_PIVOT")) e->refine_min_pivot = (float)atof(env);
     if (const char* env = getenv("ALS_DUAL_SIDE")) e->dual_side = env[0] != '0';
-    if (const char* env = getenv("ALS_DEBUG_SKIP_REFINE"))
-        if (env[0] == '1') e->debug_flags |= cfk::SOLVE_FLAG_SKIP_REFINE;
     hipError_t st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (st != hipSuccess) {
         delete e;
@@ -417,20 +424,24 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
         }
     }
     // Short rows in entry space (split-bf16 path): rows of <= 3 blocks at KP = 128, 1 block at KP = 64 solve the
-    // (padded entries)^2 system of als_solve_dual instead of the KP x KP one. ALS_DUAL=0 turns it off.
+    // (padded entries)^2 system of als_solve_dual instead of the KP x KP one. Only rows with n <= k entries: then
+    // Y Y^T + lambda n I_n has the nonzero spectrum of Y^T Y + lambda n I_k plus nothing smaller, so the same
+    // conditioning; with n > k the n x n system would carry n - k eigenvalues lambda n only (singular at
+    // lambda = 0 where the reference's k x k system is not). ALS_DUAL=0 turns it off.
     std::vector<Task> sq_all = tasks;
     std::vector<Task> dual[3];
     {
-        int max_cd = e->path != Path::MFMA_SPLIT ? 0 : e->kp == 128 ? 6 : e->kp == 64 ? 2 : 0;
-        if (const char* env = getenv("ALS_DUAL_MAX_CD")) max_cd = std::min(max_cd, atoi(env));
+        const int max_cd = e->path != Path::MFMA_SPLIT ? 0 : e->kp == 128 ? 6 : e->kp == 64 ? 2 : 0;
         bool on = max_cd > 0;
         if (const char* env = getenv("ALS_DUAL")) on = on && env[0] != '0';
         if (on) {
             std::vector<Task> keep;
             for (const Task& t : tasks) {
                 const int cd = 2 * ((t.nent + cfk::BLOCK_ENTRIES - 1) / cfk::BLOCK_ENTRIES);
-                if (t.kind == cfk::TASK_FULL && t.ndeg > 0 && cd <= max_cd) dual[cd / 2 - 1].push_back(t);
-                else keep.push_back(t);
+                if (t.kind == cfk::TASK_FULL && t.ndeg > 0 && t.ndeg <= e->k && cd <= max_cd)
+                    dual[cd / 2 - 1].push_back(t);
+                else
+                    keep.push_back(t);
             }
             tasks.swap(keep);
         }
@@ -470,15 +481,17 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
         const int64_t sb = (n_opp_rows + 1) * (int64_t)cfk::PRESPLIT_ROW_BYTES;
         bool ps = e->path == Path::MFMA_SPLIT && e->kp == 64 && sb <= (8ll << 20);
         if (const char* env = getenv("ALS_PRESPLIT")) ps = e->path == Path::MFMA_SPLIT && e->kp == 64 && env[0] == '1';
-        if (n_opp_rows + 1 >= (1 << 24)) ps = false;   // 24-bit row offsets in the pre-split gather
+        // the pre-split gather forms 32-bit byte offsets row * PRESPLIT_ROW_BYTES with a 24-bit multiply: both the
+        // row (< 2^24) and the offset (< 2^32) must fit, also when ALS_PRESPLIT=1 forces the path
+        if (n_opp_rows + 1 >= (1 << 24) || sb > (int64_t)UINT32_MAX) ps = false;
         // its RHS multiplies bf16 ratings: integers beyond +-256 are not all bf16 (257 -> 256), so such blocks
         // take the fp32 VALU RHS of the on-the-fly split path instead
         if (max_abs_rating > 256) ps = false;
         blk.presplit = ps;
         // waves per SIMD of the main launch: the pre-split Gram runs 3 (one gather buffer in 168 VGPRs, the
-        // other waves hide its latency: Netflix-shape user half 4.18 -> 3.84 ms, kbench), the other MFMA variants
-        // 2. ALS_MFMA_WAVES overrides all; ALS_SPLIT_WAVES=3 selects the one-buffer variant of the on-the-fly split.
-        blk.min_waves = e->min_waves > 0 ? e->min_waves : (ps ? 3 : e->split_waves);
+        // other waves hide its latency: Netflix-shape user half 4.18 -> 3.84 ms, kbench), the other KP <= 64 MFMA
+        // variants 2 (KP = 128: 1, fixed by the launch)
+        blk.min_waves = ps ? 3 : 2;
         if (ps && (size_t)sb > e->split_bytes) {
             (void)hipFree(e->d_split);
             e->d_split = nullptr;
@@ -734,9 +747,9 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
     const Factors& self = e->fac[side];
     const Factors& opp = e->fac[1 - side];
     if (!self.ptr || !opp.ptr) return fail(ALS_ERR_STATE, "als_solve_half: factor matrices not allocated/bound");
-    if (b.row_offset + b.n_rows > self.n_rows)
-        return fail(ALS_ERR_STATE, "block rows [%lld,%lld) exceed factor rows %lld", (long long)b.row_offset,
-                    (long long)(b.row_offset + b.n_rows), (long long)self.n_rows);
+    if (b.n_rows > 0 && b.factor_row(b.n_rows - 1) >= self.n_rows)
+        return fail(ALS_ERR_STATE, "block rows (last at factor row %lld) exceed factor rows %lld",
+                    (long long)b.factor_row(b.n_rows - 1), (long long)self.n_rows);
     if (b.n_opp_rows != opp.n_rows)   // the padding entries gather row n_opp_rows: it must be the sentinel
         return fail(ALS_ERR_STATE, "block was set for %lld opposite rows, the opposite factor matrix has %lld",
                     (long long)b.n_opp_rows, (long long)opp.n_rows);
@@ -754,6 +767,8 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
     a.opp = opp.ptr;
     a.out = self.ptr;
     a.row_offset = b.row_offset;
+    a.rows_per_chunk = (int32_t)b.rows_per_chunk;
+    a.chunk_stride = b.chunk_stride;
     a.partials = e->d_partials;
     a.lambda = lambda;
     a.sentinel = (int32_t)b.n_opp_rows;
@@ -962,6 +977,8 @@ int als_sq_error(als_engine* e, int side, double* sum_sq_error, int64_t* count) 
     a.opp = opp.ptr;
     a.self = self.ptr;
     a.row_offset = b.row_offset;
+    a.rows_per_chunk = (int32_t)b.rows_per_chunk;
+    a.chunk_stride = b.chunk_stride;
     a.task_se = b.d_task_se;
     a.sentinel = (int32_t)b.n_opp_rows;
     HIP_TRY(cfk::launch_sq_error(e->precision, e->kp, a, e->stream));
@@ -1054,6 +1071,20 @@ static int comm_streams(als_engine* e) {
     return ALS_OK;
 }
 
+// Caller-level RCCL groups (als_comm_group_start / _end, one host thread driving several engines): inside a
+// group a collective is only placed on its stream at the OUTERMOST ncclGroupEnd, so the "gathered" event of an
+// all-gather issued inside a group must be recorded after that end, not at the call (recorded earlier it would
+// order nothing). The thread's open-group depth and the (engine, side) pairs whose record is deferred:
+thread_local int g_group_depth = 0;
+thread_local std::vector<std::pair<als_engine*, int>> g_group_gathers;
+
+static int record_gathered(als_engine* e, int side) {
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipEventRecord(e->gathered[side], e->comm_stream));
+    e->gather_pending[side] = true;
+    return ALS_OK;
+}
+
 int als_comm_unique_id(void* id_out, int nbytes) {
     if (!id_out || nbytes < (int)sizeof(ncclUniqueId))
         return fail(ALS_ERR_INVALID_ARGUMENT, "unique id buffer must hold %d bytes", (int)sizeof(ncclUniqueId));
@@ -1107,48 +1138,66 @@ int als_comm_info(const als_engine* e, int* world, int* rank) {
 
 int als_comm_group_start(void) {
     NCCL_TRY(ncclGroupStart());
+    ++g_group_depth;
     return ALS_OK;
 }
 
 int als_comm_group_end(void) {
-    NCCL_TRY(ncclGroupEnd());
+    if (g_group_depth <= 0) return fail(ALS_ERR_STATE, "als_comm_group_end without als_comm_group_start");
+    const ncclResult_t r = ncclGroupEnd();
+    if (--g_group_depth > 0) {
+        if (r != ncclSuccess) return fail(ALS_ERR_COMM, "ncclGroupEnd failed: %s", ncclGetErrorString(r));
+        return ALS_OK;
+    }
+    // outermost end: the grouped all-gathers are on their streams now; record their events behind them
+    std::vector<std::pair<als_engine*, int>> touched;
+    touched.swap(g_group_gathers);
+    if (r != ncclSuccess) return fail(ALS_ERR_COMM, "ncclGroupEnd failed: %s", ncclGetErrorString(r));
+    for (auto& eg : touched)
+        if (int rc = record_gathered(eg.first, eg.second)) return rc;
     return ALS_OK;
 }
 
-int als_allgather_shard(als_engine* e, int side, int64_t slots_per_shard, int64_t slot_lo, int64_t slot_hi) {
+int als_allgather_shard(als_engine* e, int side, int64_t slots_per_chunk, int64_t chunk) {
     if (int r = check_engine(e)) return r;
     if (int r = check_side(side)) return r;
     if (e->world == 1 && !e->comm) return ALS_OK;   // one shard: the replica is the matrix
     if (!e->comm) return fail(ALS_ERR_STATE, "als_allgather_shard: no communicator (als_comm_init)");
     const Factors& f = e->fac[side];
     if (!f.ptr) return fail(ALS_ERR_STATE, "factors of side %d not allocated/bound", side);
-    const int64_t S = slots_per_shard;
-    if (S < 0 || slot_lo < 0 || slot_lo > slot_hi || slot_hi > S || S * e->world > f.n_rows)
-        return fail(ALS_ERR_INVALID_ARGUMENT, "slot range [%lld, %lld) of %lld slots per shard x %d shards vs %lld rows",
-                    (long long)slot_lo, (long long)slot_hi, (long long)S, e->world, (long long)f.n_rows);
-    if (slot_hi == slot_lo) return ALS_OK;
+    const int64_t Sc = slots_per_chunk;
+    if (Sc < 0 || chunk < 0 || (chunk + 1) * Sc * e->world > f.n_rows)
+        return fail(ALS_ERR_INVALID_ARGUMENT, "chunk %lld of %lld slots per shard x %d shards exceeds %lld rows",
+                    (long long)chunk, (long long)Sc, e->world, (long long)f.n_rows);
+    if (Sc == 0) return ALS_OK;
     HIP_TRY(hipSetDevice(e->device));
     // after this engine's solve (stream) on comm_stream; the next solve that reads this side waits for it
     HIP_TRY(hipEventRecord(e->solved, e->stream));
     HIP_TRY(hipStreamWaitEvent(e->comm_stream, e->solved, 0));
     const ncclDataType_t dt = e->precision == ALS_F64 ? ncclFloat64 : ncclFloat32;
     const size_t row = (size_t)e->kp * e->elem();
-    char* base = (char*)f.ptr;
-    const size_t count = (size_t)(slot_hi - slot_lo) * e->kp;
-    if (slot_lo == 0 && slot_hi == S) {
-        // shard-major slots: the all-gather of equal S-row shards IS the whole matrix (in place)
-        NCCL_TRY(ncclAllGather(base + (size_t)e->rank * S * row, base, count, dt, e->comm, e->comm_stream));
-    } else {
-        // rows [lo, hi) of every shard: one in-place broadcast per shard owner, grouped
-        NCCL_TRY(ncclGroupStart());
-        for (int g = 0; g < e->world; ++g) {
-            char* p = base + ((size_t)g * S + slot_lo) * row;
-            NCCL_TRY(ncclBroadcast(p, p, count, dt, g, e->comm, e->comm_stream));
-        }
-        NCCL_TRY(ncclGroupEnd());
+    // chunk-major slots: chunk c holds the G shards' Sc-row pieces back to back, so its exchange is ONE
+    // contiguous in-place all-gather
+    char* cbase = (char*)f.ptr + (size_t)chunk * (size_t)(Sc * e->world) * row;
+    NCCL_TRY(ncclAllGather(cbase + (size_t)e->rank * Sc * row, cbase, (size_t)Sc * e->kp, dt, e->comm,
+                           e->comm_stream));
+    if (g_group_depth > 0) {   // placed on the stream at the outermost group end: record the event there
+        g_group_gathers.emplace_back(e, side);
+        return ALS_OK;
     }
-    HIP_TRY(hipEventRecord(e->gathered[side], e->comm_stream));
-    e->gather_pending[side] = true;
+    return record_gathered(e, side);
+}
+
+int als_set_row_layout(als_engine* e, int side, int64_t rows_per_chunk, int64_t chunk_stride) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    Block& b = e->blk[side];
+    if (!b.set) return fail(ALS_ERR_STATE, "als_set_row_layout: no block set for side %d", side);
+    if (rows_per_chunk < 0 || (rows_per_chunk > 0 && chunk_stride < rows_per_chunk) || rows_per_chunk > INT32_MAX)
+        return fail(ALS_ERR_INVALID_ARGUMENT, "rows_per_chunk %lld / chunk_stride %lld", (long long)rows_per_chunk,
+                    (long long)chunk_stride);
+    b.rows_per_chunk = rows_per_chunk;
+    b.chunk_stride = rows_per_chunk > 0 ? chunk_stride : 0;
     return ALS_OK;
 }
 

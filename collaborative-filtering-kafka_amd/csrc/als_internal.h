@@ -60,12 +60,22 @@ struct SolveArgs {
     uint32_t* integrity;    // device record of partial slots that failed their check (see als_kernels.hip)
     float refine_min_pivot; // MFMA tile solve: skip the refinement step when every scaled pivot >= this (> 1: never)
     const uint32_t* rat_pk; // presplit: the padded ratings as bf16 pairs (entries 2i, 2i+1), exact for |r| <= 256
+    int32_t rows_per_chunk; // chunk-major slots (als_set_row_layout): 0 = factor row row_offset + row, else
+    int64_t chunk_stride;   //   row_offset + (row / rows_per_chunk) * chunk_stride + row % rows_per_chunk
 };
+// Factor row of local row `row` under the block's slot layout (wave-uniform: scalar arithmetic, once per task).
+__host__ __device__ inline int64_t factor_row(int64_t row_offset, int32_t rows_per_chunk, int64_t chunk_stride,
+                                              int32_t row) {
+    if (rows_per_chunk <= 0) return row_offset + row;
+    const int32_t q = row / rows_per_chunk;
+    return row_offset + (int64_t)q * chunk_stride + (row - q * rows_per_chunk);
+}
 // Partial-slot integrity record (device, 4 words): [0] REDUCE tasks that found a bad slot, [1] generation, [2] slot,
 // [3] row of the first failure. Read back by every synchronising call of the engine.
 constexpr int INTEGRITY_WORDS = 4;
 // Diagnostic: skip the k x k solve after the Gram (stores the Gram diagonal instead) -- used by
-// tools/kbench.py to split a launch's time into Gram and solve. Never set on the product path.
+// tools/kbench.py to split a launch's time into Gram and solve. Only the debug build (CFK_DEBUG_KNOBS) can set
+// these flags; the product library never does.
 constexpr int32_t SOLVE_FLAG_SKIP_SOLVE = 1;
 constexpr int32_t SOLVE_FLAG_SKIP_REFINE = 2;   // diagnostic: no refinement step (accuracy experiments)
 
@@ -79,6 +89,8 @@ struct SqErrArgs {
     int64_t row_offset;
     double* task_se;        // [n_tasks]
     int32_t sentinel;
+    int32_t rows_per_chunk; // slot layout as SolveArgs
+    int64_t chunk_stride;
 };
 
 // Gram paths: VALU (LDS-staged, fp32 k < 32 and all fp64), MFMA (v_mfma_f32_16x16x4_f32, exact f32

@@ -223,7 +223,7 @@ __device__ __forceinline__ void solve_store(T* P, const T* rhs_l, T* bc, const T
     const int j = lane;
     const bool act = j < KP;
     const int jr = act ? j : KP - 1;
-    T* out = (T*)a.out + (a.row_offset + tk.row) * (int64_t)KP;
+    T* out = (T*)a.out + factor_row(a.row_offset, a.rows_per_chunk, a.chunk_stride, tk.row) * (int64_t)KP;
 
     if (tk.ndeg == 0) {   // cannot occur in the reference (entities exist only once rated); defined as 0
         if (act) out[j] = T(0);
@@ -594,7 +594,7 @@ template <int C, bool DUAL = false, class TT, class KT>
 __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc)[C], float* buf, const Task& tk,
                                             const SolveArgs& a, int lane) {
     const int g = lane >> 4, j = lane & 15;
-    float* out = (float*)a.out + (a.row_offset + tk.row) * (int64_t)(16 * C);
+    float* out = (float*)a.out + factor_row(a.row_offset, a.rows_per_chunk, a.chunk_stride, tk.row) * (int64_t)(16 * C);
     auto is_real = [&](int b) { return DUAL ? logical_entry(16 * b + j) < tk.nent : C * j + b < a.k; };
     auto emit = [&](const float (&xs)[C]) {   // xs = solution in the scaled variables, times scol
         if constexpr (DUAL) {
@@ -1531,7 +1531,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
     }
 
     if (a.flags & SOLVE_FLAG_SKIP_SOLVE) {   // diagnostics (kbench): Gram only
-        float* out = (float*)a.out + (a.row_offset + tk.row) * (int64_t)KP;
+        float* out = (float*)a.out + factor_row(a.row_offset, a.rows_per_chunk, a.chunk_stride, tk.row) * (int64_t)KP;
         if (lane < 16) {
 #pragma unroll
             for (int b = 0; b < C; ++b) out[C * lane + b] = acc.g[tile_index<C>(b, b)][0] + acc.rhs[b];
@@ -1663,7 +1663,7 @@ __global__ __launch_bounds__(64 * WAVES, CD <= 4 ? 2 : 1) void als_solve_dual(So
 #pragma unroll
             for (int f = 0; f < NF; ++f) xo[f] += row[64 * f] * al;
         }
-    float* out = (float*)a.out + (a.row_offset + tk.row) * (int64_t)KP + lane;
+    float* out = (float*)a.out + factor_row(a.row_offset, a.rows_per_chunk, a.chunk_stride, tk.row) * (int64_t)KP + lane;
 #pragma unroll
     for (int f = 0; f < NF; ++f) out[64 * f] = (lane + 64 * f < a.k) ? xo[f] : 0.f;
 }
@@ -1781,7 +1781,7 @@ __global__ __launch_bounds__(256) void als_sq_error_kernel(SqErrArgs a) {
     if (tid >= a.n_tasks) return;
     const Task tk = load_task(a.tasks + tid);
     const int es = lane / LPE, v = lane % LPE;
-    const T* self = (const T*)a.self + (a.row_offset + tk.row) * (int64_t)KP;
+    const T* self = (const T*)a.self + factor_row(a.row_offset, a.rows_per_chunk, a.chunk_stride, tk.row) * (int64_t)KP;
     const T* opp = (const T*)a.opp;
     const VT x = *(const VT*)(self + v * VN);
     const int n = (tk.nsteps + BLOCK_SUBSTEPS - 1) / BLOCK_SUBSTEPS * BLOCK_ENTRIES;   // task span
@@ -1967,17 +1967,15 @@ hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s) {
 hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, int min_waves,
                         bool presplit, bool reduce) {
     if (precision == 0) {
+        // occupancy (waves per SIMD) per variant: KP <= 64 two, the pre-split KP = 64 Gram three, KP = 128 one
+        (void)min_waves;
         if (path == Path::MFMA) {
             if (kp == 32) return launch_solve_t<float, 32, Path::MFMA, 2>(a, s, reduce);
-            if (kp == 64 && min_waves >= 3) return launch_solve_t<float, 64, Path::MFMA, 3>(a, s, reduce);
             if (kp == 64) return launch_solve_t<float, 64, Path::MFMA, 2>(a, s, reduce);
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA, 1>(a, s, reduce);
         } else if (path == Path::MFMA_SPLIT) {
             if (kp == 32) return launch_solve_t<float, 32, Path::MFMA_SPLIT, 2>(a, s, reduce);
-            if (kp == 64 && presplit && min_waves >= 3)
-                return launch_solve_t<float, 64, Path::MFMA_SPLIT, 3, true>(a, s, reduce);
-            if (kp == 64 && presplit) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2, true>(a, s, reduce);
-            if (kp == 64 && min_waves >= 3) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 3>(a, s, reduce);
+            if (kp == 64 && presplit) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 3, true>(a, s, reduce);
             if (kp == 64) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2>(a, s, reduce);
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1>(a, s, reduce);
         } else {

@@ -123,6 +123,16 @@ class Dataset:
         keys = ("n_rows", "row_offset", "nnz", "slots_per_shard", "n_slots")
         return dict(zip(keys, (x.value for x in v)))
 
+    def set_slot_chunks(self, side, n_chunks: int):
+        """Chunk-major slot layout of `side` with n_chunks chunks (include/als_host.h "Slot layout")."""
+        call("als_dataset_set_slot_chunks", self._h, _side(side), int(n_chunks))
+
+    def slot_layout(self, side, n_shards=1) -> tuple[int, int]:
+        """(slots per shard and chunk Sc, chunks C) of `side` under n_shards shards."""
+        sc, c = ctypes.c_int64(), ctypes.c_int()
+        call("als_dataset_slot_layout", self._h, _side(side), n_shards, ctypes.byref(sc), ctypes.byref(c))
+        return sc.value, c.value
+
     def shard_block(self, side, n_shards=1, shard=0) -> dict:
         """In-block CSR of one shard: rows in ascending id, entries in arrival order, cols = opposite slots."""
         info = self.shard_info(side, n_shards, shard)
@@ -359,10 +369,14 @@ class ALSEngine:
         call("als_comm_info", self._h, ctypes.byref(w), ctypes.byref(r))
         return w.value, r.value
 
-    def allgather_shard(self, side, slots_per_shard: int, slot_lo: int = 0, slot_hi: int | None = None):
-        """All-gather slots [slot_lo, slot_hi) of every shard of `side` into this engine's replica."""
-        hi = slots_per_shard if slot_hi is None else slot_hi
-        call("als_allgather_shard", self._h, _side(side), slots_per_shard, slot_lo, hi)
+    def allgather_shard(self, side, slots_per_chunk: int, chunk: int = 0):
+        """All-gather chunk `chunk` of `side` (every shard's slots_per_chunk rows of it, one contiguous region of
+        the chunk-major layout) into this engine's replica; an unchunked side: its slots per shard, chunk 0."""
+        call("als_allgather_shard", self._h, _side(side), int(slots_per_chunk), int(chunk))
+
+    def set_row_layout(self, side, rows_per_chunk: int, chunk_stride: int):
+        """Local row i -> factor row row_offset + (i // rows_per_chunk) * chunk_stride + i % rows_per_chunk."""
+        call("als_set_row_layout", self._h, _side(side), int(rows_per_chunk), int(chunk_stride))
 
     def comm_wait(self):
         call("als_comm_wait", self._h)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define ALS_ABI_VERSION 2
+#define ALS_ABI_VERSION 3
 
 typedef enum {
     ALS_OK = 0,
@@ -121,22 +121,31 @@ int als_solve_half(als_engine* e, int side, float lambda);
  * input) does not change between them: chunk 0 prepares it (the pre-split copy), later chunks reuse that. */
 int als_set_chunks(als_engine* e, int side, int n_chunks, const int64_t* row_bounds);
 int als_solve_half_chunk(als_engine* e, int side, float lambda, int chunk);
+/* Chunk-major slot layout of `side`'s rows (after als_set_block, which resets it): local row i is solved into
+ * factor row row_offset + (i / rows_per_chunk) * chunk_stride + i % rows_per_chunk (rows_per_chunk = 0: the
+ * contiguous row_offset + i). With Sc = rows_per_chunk and chunk_stride = G Sc, the rows of chunk c of every
+ * shard are contiguous (als_host.h "Slot layout"). */
+int als_set_row_layout(als_engine* e, int side, int64_t rows_per_chunk, int64_t chunk_stride);
 
 /* ---- multi-GPU: shards + RCCL all-gather over xGMI ------------------------------------------------
  * Replaces the per-iteration feature topics (ALSApp.java:105-151): entities are sharded by raw id % G
- * (PureModStreamPartitioner.java:9-10) into shard-major slots (slot = shard * S + rank in shard, S = slots per
- * shard), every engine holds its shard's in-blocks and a full replica of both factor matrices, and each half
- * ends with one all-gather of the updated shard. One engine per GPU; either one process per GPU (unique id from
+ * (PureModStreamPartitioner.java:9-10) into chunk-major slots (als_host.h "Slot layout": slot = (r / Sc) G Sc +
+ * shard Sc + r % Sc for rank r in the shard, Sc = slots per shard and chunk; one chunk: slot = shard S + r), every
+ * engine holds its shard's in-blocks and a full replica of both factor matrices, and each half ends with one
+ * all-gather per chunk of the updated shard. One engine per GPU; either one process per GPU (unique id from
  * als_comm_unique_id on one process, shared by the caller, then als_comm_init on every process) or one process
  * driving G GPUs (als_comm_init_group). The exchange is enqueued on the engine's stream after its solve. */
 int als_comm_unique_id(void* id_out, int nbytes);   /* nbytes >= 128 */
 int als_comm_init(als_engine* e, int world, int rank, const void* unique_id);
 int als_comm_init_group(als_engine** engines, int n);
 int als_comm_info(const als_engine* e, int* world, int* rank);
-/* Gather slots [slot_lo, slot_hi) of every shard of `side` (all of them: slot_lo = 0, slot_hi = S) into every
- * engine's replica. A single host thread driving several engines wraps its per-engine calls in
- * als_comm_group_start / als_comm_group_end. A no-op for an engine without a communicator (G = 1). */
-int als_allgather_shard(als_engine* e, int side, int64_t slots_per_shard, int64_t slot_lo, int64_t slot_hi);
+/* Gather chunk `chunk` of `side` -- factor rows [chunk G Sc, (chunk + 1) G Sc), this engine's Sc rows at
+ * chunk G Sc + rank Sc -- into every engine's replica: one in-place ncclAllGather (Sc = slots_per_chunk; an
+ * unchunked side passes its S slots per shard and chunk 0). A single host thread driving several engines
+ * wraps its per-engine calls in als_comm_group_start / als_comm_group_end; the engines' completion events are
+ * then recorded at the outermost group end, where RCCL places the grouped collectives on their streams. A no-op
+ * for an engine without a communicator (G = 1). */
+int als_allgather_shard(als_engine* e, int side, int64_t slots_per_chunk, int64_t chunk);
 int als_comm_group_start(void);
 int als_comm_group_end(void);
 /* The all-gathers run on the engine's own communication stream, after the solve that produced the shard and

@@ -10,11 +10,14 @@
  *   - output:   FeatureCollector.calculatePredictionMatrix + EJML MatrixIO.saveDenseCSV   processors/FeatureCollector.java:72-110
  * plus the seeded synthetic Netflix-shape generator used by the benchmark (BASELINE.json configs[2]).
  *
- * Slot layout for G shards (G = 1 for one GPU): entities of a side are sharded by raw_id % G; inside a
- * shard they are ordered by ascending raw id; slot = shard * S + rank_in_shard with S = the largest shard
- * size. The factor matrix of a side has G * S rows in slot order, so an all-gather of equal S-row shards
- * IS the full matrix. For G = 1, slot = rank of the raw id among all ids of that side (= the collector's
- * TreeMap order, FeatureCollector.java:21-22).
+ * Slot layout for G shards (G = 1 for one GPU) and C chunks (default 1): entities of a side are sharded by
+ * raw_id % G; inside a shard they are ordered by ascending raw id (rank r = the entity's local row in its
+ * shard's block). With S = the largest shard size and Sc = ceil(S / C) slots per shard and chunk,
+ *     slot = (r / Sc) * (G * Sc) + shard * Sc + r % Sc            ("chunk-major")
+ * so chunk c of the factor matrix (rows [c G Sc, (c+1) G Sc)) holds the G shards' Sc-row pieces back to back,
+ * and the exchange of one chunk after it is solved is ONE contiguous all-gather (als_allgather_shard). C = 1
+ * gives slot = shard * S + r: the all-gather of equal S-row shards IS the full matrix. For G = 1, slot = rank of
+ * the raw id among all ids of that side (= the collector's TreeMap order, FeatureCollector.java:21-22).
  */
 #ifndef CFK_ALS_HOST_H
 #define CFK_ALS_HOST_H
@@ -59,10 +62,16 @@ int als_dataset_ratings(const als_dataset* ds, int32_t* movie_ids, int32_t* user
  * never fires for such an entity, so the reference hangs; callers reject them (ALS_ERR_DATA). */
 int als_dataset_count_duplicates(const als_dataset* ds, int64_t* n_dup);
 
-/* Shard `shard` of `side` under G = n_shards: rows, the shard's first slot, its entry count, slots per
- * shard (S) and total slots (G * S) of this side. */
+/* Shard `shard` of `side` under G = n_shards: rows, the shard's first slot (shard * Sc), its entry count, the
+ * slots a shard owns (C * Sc, >= its rows) and total slots (G * C * Sc) of this side. */
 int als_dataset_shard_info(const als_dataset* ds, int side, int n_shards, int shard, int64_t* n_rows,
                            int64_t* row_offset, int64_t* nnz, int64_t* slots_per_shard, int64_t* n_slots);
+/* Chunk count C of `side`'s slot layout (default 1); affects every later slot query of that side (and the
+ * opposite side's column indices). */
+int als_dataset_set_slot_chunks(als_dataset* ds, int side, int n_chunks);
+/* Sc (slots per shard and chunk) and C of `side` under G = n_shards: local row i of a shard's block sits at
+ * slot row_offset + (i / Sc) * (G * Sc) + i % Sc (als_set_row_layout(e, side, Sc, G * Sc)). */
+int als_dataset_slot_layout(const als_dataset* ds, int side, int n_shards, int64_t* slots_per_chunk, int* n_chunks);
 /* The shard's in-block CSR: row_ptr[n_rows+1], col_idx[nnz] = opposite-side SLOTS under the same G,
  * ratings[nnz], row_ids[n_rows] = raw ids (any of col/ratings/row_ids may be NULL). */
 int als_dataset_shard_block(const als_dataset* ds, int side, int n_shards, int64_t shard, int64_t* row_ptr,

@@ -13,7 +13,8 @@ import static java.lang.foreign.ValueLayout.JAVA_INT;
 import static java.lang.foreign.ValueLayout.JAVA_LONG;
 
 /**
- * Panama FFM (Java 22+) binding of libcfk_als.so, the C ABI declared in include/als.h. No native shim: every
+ * Panama FFM (Java 22+) binding of libcfk_als.so, the C ABI declared in include/als.h (the processors under
+ * processors/ use the JNI binding AlsNative, which runs on the reference's Java 13). No native shim: every
  * downcall handle below binds one exported symbol with the descriptor of its C prototype
  * (int -> JAVA_INT, int64_t -> JAVA_LONG, float -> JAVA_FLOAT, any pointer -> ADDRESS).
  * tests/test_integration_java.py checks each descriptor against the library's ctypes signatures.
@@ -72,7 +73,9 @@ public final class AlsFfm {
     static final MethodHandle COMM_INIT = h("als_comm_init",
             FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT, ADDRESS));
     static final MethodHandle ALLGATHER_SHARD = h("als_allgather_shard",
-            FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_LONG, JAVA_LONG, JAVA_LONG));
+            FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_LONG, JAVA_LONG));
+    static final MethodHandle SET_ROW_LAYOUT = h("als_set_row_layout",
+            FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_LONG, JAVA_LONG));
     static final MethodHandle COMM_WAIT = h("als_comm_wait", FunctionDescriptor.of(JAVA_INT, ADDRESS));
     // ---- collector, MSE, synchronisation (als.h:153-166)
     static final MethodHandle PREDICT = h("als_predict",
@@ -201,9 +204,19 @@ public final class AlsFfm {
         }
     }
 
-    public static void allgatherShard(MemorySegment e, int side, long slotsPerShard, long lo, long hi) {
+    /** Chunk `chunk` of the side's chunk-major slots (an unchunked side: its slots per shard, chunk 0). */
+    public static void allgatherShard(MemorySegment e, int side, long slotsPerChunk, long chunk) {
         try {
-            check("als_allgather_shard", (int) ALLGATHER_SHARD.invokeExact(e, side, slotsPerShard, lo, hi));
+            check("als_allgather_shard", (int) ALLGATHER_SHARD.invokeExact(e, side, slotsPerChunk, chunk));
+        } catch (Throwable t) {
+            throw rethrow(t);
+        }
+    }
+
+    /** Local row i -> factor row rowOffset + (i / rowsPerChunk) * chunkStride + i % rowsPerChunk. */
+    public static void setRowLayout(MemorySegment e, int side, long rowsPerChunk, long chunkStride) {
+        try {
+            check("als_set_row_layout", (int) SET_ROW_LAYOUT.invokeExact(e, side, rowsPerChunk, chunkStride));
         } catch (Throwable t) {
             throw rethrow(t);
         }

@@ -188,7 +188,7 @@ DEFINE_LU_INVERT(double, f64, fabs)
         _Pragma("omp parallel num_threads(nthreads > 0 ? nthreads : 1)")                                 \
         {                                                                                                \
             T* ws = (T*)malloc(ws_bytes);                                                                \
-            _Pragma("omp for schedule(dynamic, 8)")                                                     \
+            _Pragma("omp for schedule(dynamic, 1)")                                                     \
             for (int64_t r = 0; r < n_rows; ++r)                                                         \
                 update_row_##SUFFIX(row_ptr[r], row_ptr[r + 1], col_idx, ratings, opp, k, lam,           \
                                     out + r * (int64_t)k, ws);                                           \

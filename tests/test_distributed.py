@@ -27,6 +27,17 @@ class OracleShardEngine:
         self.dtype = torch.float64
         self.factors = [None, None]
         self.blocks = [None, None]
+        self.layout = [(0, 0), (0, 0)]
+
+    def set_row_layout(self, side, rows_per_chunk, chunk_stride):
+        self.layout[side] = (int(rows_per_chunk), int(chunk_stride))
+
+    def _rows(self, side, lo, hi):
+        """factor rows of local rows [lo, hi) under the side's slot layout (als_set_row_layout)"""
+        off = self.blocks[side][3]
+        i = np.arange(lo, hi)
+        rpc, stride = self.layout[side]
+        return off + i if rpc == 0 else off + (i // rpc) * stride + i % rpc
 
     def use_torch_stream(self):
         pass
@@ -54,7 +65,7 @@ class OracleShardEngine:
         opp = self.factors[1 - side][:n_opp].numpy()
         s = self.oracle.Side(ids=np.arange(len(rp) - 1), row_ptr=rp, col=col, ratings=rat)
         out = self.oracle.update_side(s, opp, lam, "f64", 1)
-        self.factors[side][off:off + len(out)] = torch.from_numpy(out)
+        self.factors[side][self._rows(side, 0, len(out))] = torch.from_numpy(out)
 
     def set_chunks(self, side, bounds):
         self.chunks = [(int(bounds[c]), int(bounds[c + 1])) for c in range(len(bounds) - 1)]
@@ -66,12 +77,13 @@ class OracleShardEngine:
         sub = rp[lo:hi + 1] - rp[lo]
         s = self.oracle.Side(ids=np.arange(hi - lo), row_ptr=sub, col=col[rp[lo]:rp[hi]], ratings=rat[rp[lo]:rp[hi]])
         out = self.oracle.update_side(s, opp, lam, "f64", 1)
-        self.factors[side][off + lo:off + hi] = torch.from_numpy(out)
+        self.factors[side][self._rows(side, lo, hi)] = torch.from_numpy(out)
 
     def sq_error(self, side):
         rp, col, rat, off, n_opp = self.blocks[0]
         s = self.oracle.Side(ids=np.arange(len(rp) - 1), row_ptr=rp, col=col, ratings=rat)
-        return self.oracle.sq_error(s, self.factors[0][off:off + len(rp) - 1].numpy(), self.factors[1][:n_opp].numpy())
+        rows = self._rows(0, 0, len(rp) - 1)
+        return self.oracle.sq_error(s, self.factors[0][rows].numpy(), self.factors[1][:n_opp].numpy())
 
 
 def _worker(rank, world, port, path, out_dir, chunks=4):
@@ -103,8 +115,8 @@ def _free_port():
 
 @pytest.mark.parametrize("world,chunks", [(2, 1), (2, 4), (3, 3), (4, 7)])
 def test_sharded_driver_matches_single_process(cfk, oracle_mod, tiny_path, tmp_path, world, chunks):
-    """chunks > 1: the user half is solved in row-range chunks whose all-gathers (async, list form) overlap
-    the next chunk's solve."""
+    """chunks > 1: the user half is solved in row-range chunks over chunk-major user slots; each chunk's
+    all-gather (async, one contiguous all_gather_into_tensor) overlaps the next chunk's solve."""
     import torch.multiprocessing as mp
     mp.spawn(_worker, args=(world, _free_port(), tiny_path, str(tmp_path), chunks), nprocs=world, join=True)
     m, u, r = oracle_mod.parse_netflix(tiny_path)

@@ -6,9 +6,14 @@
   users and random rows -- against the fp64 oracle (oracle.update_rows_f64, the restatement of
   MFeatureCalculator.java:66-104 / UFeatureCalculator.java:66-104) and the oracle's fp32 EJML-order restatement
   (the reference's own fp32 error envelope).
-- configs[4] scaled down: one shard (G = 8) of a power-law matrix whose heaviest items carry >= 100k ratings,
-  with full factor replicas, on one GPU.
-- configs[3]: k = 128 sharded over two ranks with the chunked (overlapped) user half, against the oracle's MSE.
+- configs[3]: the same full Netflix-shape workload at k = 128 (KP = 128 variants: 36-tile split Gram, LDS tile
+  solve, entry-space solve of rows of 1-3 padded blocks), sampled rows incl. the longest split rows and rows of
+  every entry-space size; and k = 128 sharded over two ranks with the chunked (overlapped) user half at test size.
+- configs[4] at FULL size: the 10M x 1M x 2B power-law matrix, shard 0 of G = 8 (both in-blocks of the shard plus
+  full factor replicas on one GPU, exactly one rank's work of the 8-GPU job), with the heaviest items (millions of
+  ratings, 100+ partial slots each) against the oracle; and a 1/40-scale shard.
+Progress of the long tests goes to gpurun_out/fullscale_progress.log (a GPU run that prints nothing for minutes
+looks hung).
 """
 import os
 
@@ -53,6 +58,14 @@ def _check_rows(oracle_mod, blk, rows, got, opp, what):
     return float(rel.max())
 
 
+def _progress(msg):
+    from conftest import ROOT
+    d = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "fullscale_progress.log"), "a") as f:
+        f.write(msg + "\n")
+
+
 def _sample(blk, rng, n_long=20, n_rand=160, extra=()):
     deg = np.diff(blk["row_ptr"])
     longest = np.argsort(-deg, kind="stable")[:n_long]
@@ -60,26 +73,89 @@ def _sample(blk, rng, n_long=20, n_rand=160, extra=()):
     return np.unique(np.concatenate([longest, rand, np.asarray(extra, np.int64)])).astype(np.int64)
 
 
-def test_netflix_shape_full_size_sampled_rows(cfk, oracle_mod):
-    """BASELINE configs[2] at full size through ALSApp (GPU block build, split rows, pre-split user half)."""
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("k", [64, 128])
+def test_netflix_shape_full_size_sampled_rows(cfk, oracle_mod, k):
+    """BASELINE configs[2] (k = 64) and configs[3] (k = 128) at full size through ALSApp (GPU block build, split
+    rows at chunk = nnz/4096 with ~974 REDUCE rows, pre-split user half at k = 64, entry-space short rows)."""
     ds = cfk.Dataset.synthetic_netflix(480_189, 17_770, 100_000_000, 0xA15, nthreads=16)
-    app = cfk.ALSApp(1, 64, LAM, 1, precision="f32", seed=42).setup(ds, check_duplicates=False)
+    app = cfk.ALSApp(1, k, LAM, 1, precision="f32", seed=42).setup(ds, check_duplicates=False)
     eng = app.engine
     assert eng.block_stats(0)["n_reduce"] > 0                 # the real work plan has split rows
-    U0 = ds.init_user_factors(64, 42)
+    U0 = ds.init_user_factors(k, 42)
     app.movie_half()
     M = eng.read_factors(0)
     app.user_half()
     U = eng.read_factors(1)
     assert eng.integrity_status() == [0, 0, 0, 0]
+    _progress(f"netflix k={k}: halves done")
     rng = np.random.default_rng(2024)
     mblk = ds.shard_block(0)
-    worst_m = _check_rows(oracle_mod, mblk, _sample(mblk, rng), M, U0, "movie")
+    n_long = 20 if k == 64 else 12
+    worst_m = _check_rows(oracle_mod, mblk, _sample(mblk, rng, n_long=n_long), M, U0, "movie")
+    _progress(f"netflix k={k}: movie rows checked")
     ublk = ds.shard_block(1)
     udeg = np.diff(ublk["row_ptr"])
-    ones = np.nonzero(udeg == 1)[0][:40]
-    worst_u = _check_rows(oracle_mod, ublk, _sample(ublk, rng, extra=ones), U, M, "user")
-    print(f"configs[2] full size: worst norm-rel movie {worst_m:.2e}, user {worst_u:.2e}")
+    # the entry-space sizes: 1, 2 and 3 padded blocks (k = 128 solves all three in entry space, k = 64 the first)
+    extra = np.concatenate([np.nonzero(udeg == 1)[0][:40]] +
+                           [rng.choice(np.nonzero((udeg > 32 * c) & (udeg <= 32 * (c + 1)))[0], 40, replace=False)
+                            for c in range(3)])
+    dual = eng.block_path(1)["dual_rows_by_blocks"]
+    assert dual[0] > 0 and (k == 64 or min(dual) > 0), dual
+    worst_u = _check_rows(oracle_mod, ublk, _sample(ublk, rng, extra=extra), U, M, "user")
+    print(f"configs[{2 if k == 64 else 3}] full size k={k}: worst norm-rel movie {worst_m:.2e}, user {worst_u:.2e}")
+
+
+@pytest.mark.timeout(900)
+def test_powerlaw_full_2b_shard0_of_8(cfk, oracle_mod):
+    """BASELINE configs[4] at full size: 10M users x 1M items x 2B ratings (log-normal sigma 1.5 users, Zipf items),
+    shard 0 of G = 8 -- its ~250M-rating item and user in-blocks plus full factor replicas (U: 10M x 64) on one
+    GPU, i.e. one rank's work of the 8-GPU job (MFeatureCalculator.java:66-104 over the heaviest items of the
+    stress config). Checked against the fp64 oracle: the heaviest items (>= 1M ratings each, split into 100+
+    PARTIAL chunks + a REDUCE task), random items, the longest and random users."""
+    import time
+    G = 8
+    t0 = time.time()
+    ds = cfk.Dataset.synthetic_powerlaw(10_000_000, 1_000_000, 2_000_000_000, 0xA15, nthreads=16)
+    _progress(f"powerlaw 2B: generated in {time.time() - t0:.0f} s")
+    eng = cfk.ALSEngine(64, "f32")
+    info = [ds.shard_info(s, G, 0) for s in (0, 1)]
+    for side in (0, 1):
+        c = ds.shard_coo(side, G, 0)
+        eng.alloc_factors(side, info[side]["n_slots"])
+        eng.set_block_coo(side, c["n_rows"], c["rows"], c["cols"], c["ratings"], c["row_offset"],
+                          info[1 - side]["n_slots"])
+        del c
+    _progress(f"powerlaw 2B: shard 0 blocks on the GPU at {time.time() - t0:.0f} s")
+    assert eng.block_stats(0)["n_reduce"] > 0
+    U0 = ds.init_user_factors(64, 42, G)                       # slot order of G shards, 10M x 64
+    eng.write_factors(1, U0)
+    eng.solve_half(0, LAM)
+    Mfull = eng.read_factors(0)
+    M = Mfull[info[0]["row_offset"]:info[0]["row_offset"] + info[0]["n_rows"]]
+    mblk = ds.shard_block(0, G, 0)
+    mdeg = np.diff(mblk["row_ptr"])
+    heavy = np.nonzero(mdeg >= 1_000_000)[0]
+    assert len(heavy) >= 4 and mdeg.max() >= 4_000_000, (len(heavy), int(mdeg.max()))
+    rng = np.random.default_rng(7)
+    pick = np.concatenate([np.argsort(-mdeg, kind="stable")[:8], rng.choice(heavy, min(8, len(heavy)), replace=False)])
+    _progress(f"powerlaw 2B: item half solved at {time.time() - t0:.0f} s; {len(heavy)} items >= 1M ratings")
+    worst_m = _check_rows(oracle_mod, mblk, _sample(mblk, rng, n_long=0, n_rand=120, extra=pick), M, U0, "item")
+    _progress(f"powerlaw 2B: item rows checked at {time.time() - t0:.0f} s")
+    del mblk, U0
+    # user half of the shard against a random full item replica
+    Mr = rng.random((info[0]["n_slots"], 64), dtype=np.float32)
+    eng.write_factors(0, Mr)
+    eng.solve_half(1, LAM)
+    Ufull = eng.read_factors(1)
+    U = Ufull[info[1]["row_offset"]:info[1]["row_offset"] + info[1]["n_rows"]]
+    ublk = ds.shard_block(1, G, 0)
+    worst_u = _check_rows(oracle_mod, ublk, _sample(ublk, rng, n_long=20, n_rand=200), U, Mr, "user")
+    assert eng.integrity_status() == [0, 0, 0, 0]
+    eng.close()
+    _progress(f"powerlaw 2B: done at {time.time() - t0:.0f} s")
+    print(f"configs[4] full 2B, shard 0 of 8: heaviest item {mdeg.max()} ratings, {len(heavy)} items >= 1M; worst "
+          f"norm-rel item {worst_m:.2e}, user {worst_u:.2e}")
 
 
 def test_powerlaw_shard_sampled_rows(cfk, oracle_mod):

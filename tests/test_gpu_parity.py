@@ -443,50 +443,200 @@ def test_engine_ordered_with_torch_default_stream(cfk):
 
 def test_native_rccl_exchange_world1(cfk, oracle_mod):
     """The C-ABI exchange (als_comm_unique_id / als_comm_init / als_allgather_shard, RCCL) on a one-rank
-    communicator: the all-gather of whole shards and of slot ranges leaves the replicas bitwise unchanged, and
-    the chunked user half with an all-gather after every chunk (on the engine's comm stream, overlapping the
-    next chunk) reproduces als_solve_half exactly. The N > 1 exchange runs on the driver's multi-GPU node."""
+    communicator: the all-gather of the whole shard and of single chunks leaves the replicas bitwise unchanged,
+    and the chunked user half over chunk-major slots (als_set_row_layout) with an all-gather after every chunk
+    (on the engine's comm stream, overlapping the next chunk) reproduces als_solve_half exactly. The N > 1
+    exchange runs on the driver's multi-GPU node (test_comm_init_group_two_gpus where one exists)."""
     ds, b = _synthetic(cfk, oracle_mod)
+    ds.set_slot_chunks(1, 3)                              # user slots in 3 chunks (world 1: identity layout)
     eng = cfk.ALSEngine(64, "f32")
     uid = cfk.ALSEngine.comm_unique_id()
     assert len(uid) == 128
     eng.comm_init(1, 0, uid)
     assert eng.comm_info() == (1, 0)
     info = [ds.shard_info(s) for s in (0, 1)]
+    sc, nc = ds.slot_layout(1)
+    assert nc == 3 and info[1]["n_slots"] == 3 * sc >= info[1]["n_rows"]
     for side in (0, 1):
         c = ds.shard_coo(side)
         eng.alloc_factors(side, info[side]["n_slots"])
         eng.set_block_coo(side, c["n_rows"], c["rows"], c["cols"], c["ratings"], 0, info[1 - side]["n_slots"])
+    eng.set_row_layout(1, sc, sc)
     eng.write_factors(1, ds.init_user_factors(64, 3))
     eng.solve_half(0, LAM)
     M = eng.read_factors(0)
     eng.allgather_shard(0, info[0]["slots_per_shard"])
-    eng.allgather_shard(0, info[0]["slots_per_shard"], 5, 17)
+    eng.allgather_shard(0, 6, 2)                          # rows [12, 18)
     assert np.array_equal(eng.read_factors(0), M)
     eng.solve_half(1, LAM)
     U = eng.read_factors(1)
     n = info[1]["n_rows"]
-    bounds = [0, n // 3, 2 * n // 3, n]
+    bounds = [0, min(sc, n), min(2 * sc, n), n]
     eng.set_chunks(1, bounds)
     for c in range(3):
         eng.solve_half_chunk(1, LAM, c)
-        eng.allgather_shard(1, info[1]["slots_per_shard"], bounds[c], bounds[c + 1])
+        eng.allgather_shard(1, sc, c)
     assert np.array_equal(eng.read_factors(1), U)
     eng.solve_half(0, LAM)             # reads U: ordered after the pending all-gathers of the user side
     M2 = eng.read_factors(0)
     eng.close()
-    ref = oracle_mod.update_side(b.movie, U.astype(np.float64), LAM, "f64")
+    ref = oracle_mod.update_side(b.movie, U[:n].astype(np.float64), LAM, "f64")
     assert np.linalg.norm(M2 - ref) / np.linalg.norm(ref) < 1e-4
+
+
+def test_row_layout_scatters_rows_into_chunk_major_slots(cfk, oracle_mod):
+    """als_set_row_layout: local row i is solved into row_offset + (i // Sc) * stride + i % Sc -- the slots of
+    shard `row_offset / Sc` in a chunk-major layout of `stride / Sc` shards -- and every other row is untouched."""
+    ds, b = _synthetic(cfk, oracle_mod)
+    blk = ds.shard_block(1)
+    n = blk["n_rows"]
+    F = np.random.default_rng(8).random((len(b.movie.ids), 64)).astype(np.float32)
+    whole = _one_half(cfk, 1, blk, F, 64, "f32", len(b.movie.ids))
+    G, shard, sc = 3, 1, -(-n // 4)                       # 4 chunks of a 3-shard layout, this is shard 1
+    eng = cfk.ALSEngine(64, "f32")
+    eng.alloc_factors(0, len(b.movie.ids))
+    eng.alloc_factors(1, 4 * G * sc)
+    eng.set_block(1, blk["row_ptr"], blk["col"], blk["ratings"], shard * sc, len(b.movie.ids))
+    eng.set_row_layout(1, sc, G * sc)
+    eng.write_factors(0, F)
+    eng.write_factors(1, np.full((4 * G * sc, 64), 7.0, np.float32))
+    eng.solve_half(1, LAM)
+    got = eng.read_factors(1)
+    se, cnt = eng.sq_error(1)
+    eng.close()
+    i = np.arange(n)
+    rows = shard * sc + (i // sc) * G * sc + i % sc
+    assert np.array_equal(got[rows], whole)
+    others = np.setdiff1d(np.arange(4 * G * sc), rows)
+    assert np.all(got[others] == 7.0)
+    se_o, cnt_o = oracle_mod.sq_error(b.user, whole.astype(np.float64), F.astype(np.float64))
+    assert cnt == cnt_o and se == pytest.approx(se_o, rel=1e-4)
 
 
 def test_comm_init_group_one_engine(cfk):
     e = cfk.ALSEngine(16, "f32")
     cfk.ALSEngine.comm_init_group([e])
     assert e.comm_info() == (1, 0)
-    from cfk_amd._lib import ALSError
+    from cfk_amd._lib import ALSError, call
     with pytest.raises(ALSError, match="ALS_ERR_STATE"):
         cfk.ALSEngine.comm_init_group([e])            # already has a communicator
+    with pytest.raises(ALSError, match="ALS_ERR_STATE"):
+        call("als_comm_group_end")                     # no open group
     e.close()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs 2 GPUs (one engine per device)")
+def test_comm_init_group_two_gpus(cfk, oracle_mod):
+    """One host thread driving G = 2 engines through als_comm_init_group, every half's all-gathers grouped
+    (als_comm_group_start / _end: the completion events are recorded at the outermost group end): the factors
+    equal the one-GPU run's. Chunk-major user slots, 2 chunks, all-gathers after each chunk."""
+    from cfk_amd._lib import call
+    ds, b = _synthetic(cfk, oracle_mod)
+    G, iters = 2, 3
+    ds.set_slot_chunks(1, 2)
+    engs = [cfk.ALSEngine(64, "f32", device=g) for g in range(G)]
+    cfk.ALSEngine.comm_init_group(engs)
+    info = [[ds.shard_info(s, G, g) for s in (0, 1)] for g in range(G)]
+    sc = {s: ds.slot_layout(s, G)[0] for s in (0, 1)}
+    for g, e in enumerate(engs):
+        torch.cuda.set_device(g)
+        for side in (0, 1):
+            c = ds.shard_coo(side, G, g)
+            e.alloc_factors(side, info[g][side]["n_slots"])
+            e.set_block_coo(side, c["n_rows"], c["rows"], c["cols"], c["ratings"], c["row_offset"],
+                            info[g][1 - side]["n_slots"])
+        e.set_row_layout(1, sc[1], G * sc[1])
+        n = info[g][1]["n_rows"]
+        e.set_chunks(1, [0, min(sc[1], n), n])
+        e.write_factors(1, ds.init_user_factors(64, 9, G))
+    torch.cuda.set_device(0)
+    for _ in range(iters):
+        for e in engs:
+            e.solve_half(0, LAM)
+        call("als_comm_group_start")
+        for e in engs:
+            e.allgather_shard(0, sc[0], 0)
+        call("als_comm_group_end")
+        for c in range(2):
+            for e in engs:
+                e.solve_half_chunk(1, LAM, c)
+            call("als_comm_group_start")
+            for e in engs:
+                e.allgather_shard(1, sc[1], c)
+            call("als_comm_group_end")
+    U = [e.read_factors(1) for e in engs]
+    M = [e.read_factors(0) for e in engs]
+    for e in engs:
+        e.close()
+    assert np.array_equal(U[0], U[1]) and np.array_equal(M[0], M[1])
+    app = cfk.ALSApp(1, 64, LAM, iters, precision="f32", seed=9).setup(
+        cfk.Dataset.synthetic_netflix(n_users=3000, n_movies=400, nnz=90_000, seed=11, nthreads=8))
+    app.run()
+    U1, M1 = app.factors()
+    assert np.array_equal(U[0][ds.slots(1, G)], U1) and np.array_equal(M[0][ds.slots(0, G)], M1)
+
+
+def test_gram_variants_vs_oracle(cfk, oracle_mod, monkeypatch):
+    """The two knobs that select other product code paths: ALS_GRAM=f32 (exact v_mfma_f32_16x16x4_f32 Gram
+    instead of the split-bf16 one) at k = 64 and 128 against the fp64 oracle, and ALS_DUAL_SIDE=0 (entry-space
+    launches on the engine stream instead of the side stream) bitwise equal to the default."""
+    ds, b = _synthetic(cfk, oracle_mod)
+    blk = ds.shard_block(1)
+    for k in (64, 128):
+        F = np.random.default_rng(k).random((len(b.movie.ids), k))
+        ref = oracle_mod.update_side(b.user, F, LAM, "f64")
+        ref32 = oracle_mod.update_side(b.user, F.astype(np.float32), LAM, "f32")
+        outs = {}
+        for env in ({}, {"ALS_GRAM": "f32"}, {"ALS_DUAL_SIDE": "0"}):
+            for name in ("ALS_GRAM", "ALS_DUAL_SIDE"):
+                monkeypatch.delenv(name, raising=False)
+            for name, v in env.items():
+                monkeypatch.setenv(name, v)
+            outs[tuple(env.items())] = _one_half(cfk, 1, blk, F.astype(np.float32), k, "f32", len(b.movie.ids))
+        norm = np.linalg.norm(ref, axis=1)
+        rel_ref = np.linalg.norm(ref32 - ref, axis=1) / norm
+        for got in outs.values():
+            rel = np.linalg.norm(got - ref, axis=1) / norm
+            assert np.percentile(rel, 99) <= max(2 * np.percentile(rel_ref, 99), 2e-5), k
+            assert rel.max() <= max(3 * rel_ref.max(), 1e-4), k
+        assert np.array_equal(outs[()], outs[(("ALS_DUAL_SIDE", "0"),)]), k
+
+
+def test_entry_space_only_for_rows_not_longer_than_k(cfk, oracle_mod):
+    """k = 80 (KP = 128): rows of up to 3 padded blocks qualify for the entry-space solve by length, but one with
+    n > k entries would make the n x n system rank-deficient up to lambda n I: those rows take the
+    k x k path. Rows of 65..96 ratings are checked against the oracle, and the plan counts them out of the
+    entry-space launches."""
+    rng = np.random.default_rng(80)
+    n_movies, k = 300, 80
+    degs = np.concatenate([rng.integers(65, 97, 150), rng.integers(1, 80, 150)])
+    mids, uids, rats = [], [], []
+    for u, d in enumerate(degs):
+        ms = rng.choice(n_movies, size=int(d), replace=False)
+        mids += (ms + 1).tolist()
+        uids += [u + 1] * int(d)
+        rats += rng.integers(1, 6, int(d)).tolist()
+    ds = cfk.Dataset.from_ratings(np.array(mids), np.array(uids), np.array(rats))
+    m, u, r = ds.ratings()
+    b = oracle_mod.build_blocks(m, u, r)
+    blk = ds.shard_block(1)
+    F = rng.random((len(b.movie.ids), k))
+    eng = cfk.ALSEngine(k, "f32")
+    eng.alloc_factors(0, len(b.movie.ids))
+    eng.alloc_factors(1, blk["n_rows"])
+    eng.set_block(1, blk["row_ptr"], blk["col"], blk["ratings"], 0, len(b.movie.ids))
+    deg = np.diff(blk["row_ptr"])
+    assert eng.block_path(1)["dual_rows"] == int(np.sum((deg <= k) & (deg <= 96)))
+    eng.write_factors(0, F.astype(np.float32))
+    eng.solve_half(1, LAM)
+    got = eng.read_factors(1)
+    eng.close()
+    ref = oracle_mod.update_side(b.user, F, LAM, "f64")
+    ref32 = oracle_mod.update_side(b.user, F.astype(np.float32), LAM, "f32")
+    norm = np.linalg.norm(ref, axis=1)
+    rel = np.linalg.norm(got - ref, axis=1) / norm
+    rel_ref = np.linalg.norm(ref32 - ref, axis=1) / norm
+    assert rel.max() <= max(3 * rel_ref.max(), 1e-4), (rel.max(), rel_ref.max())
 
 
 @pytest.mark.parametrize("k", [64, 128])

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol(cfk):
     nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
     for name in declared:
         assert re.search(rf"\bT {name}\b", nm), name
-    assert L.als_abi_version() == 2
+    assert L.als_abi_version() == 3
 
 
 def test_kernels_are_gfx950_code_objects(cfk):

@@ -1,12 +1,22 @@
-"""The Java side of the boundary (row f3): the Panama FFM binding and the re-plumbed processor under integration/java.
+"""The Java side of the boundary (row f3): the JNI binding (AlsNative.java + integration/jni/cfk_als_jni.c, the
+reference's Java 13), the Panama FFM binding (AlsFfm.java, Java 22+), the re-plumbed processors and the topology
+under integration/java.
 
-There is no JDK in this image, so the Java is not compiled here. What is checked (CPU only):
+There is no JDK in this image, so neither the Java nor the JNI shim (it needs jni.h) is compiled here. What is
+checked (CPU only):
 - every downcall descriptor in AlsFfm.java matches the C prototype: the library's ctypes signatures
   (_lib.SIGNATURES, themselves checked against the exports in test_host.py), int -> JAVA_INT,
   int64_t -> JAVA_LONG, float -> JAVA_FLOAT, pointers -> ADDRESS;
 - every bound symbol is declared in include/als.h or include/als_host.h and exported by libcfk_als.so;
-- the re-plumbed MFeatureCalculator keeps the reference's stores, sinks and dependent-id filter
-  (processors/MFeatureCalculator.java:32-34, :117-131) and calls the hot path once per half.
+- JNI: every `native` method of AlsNative has exactly one C function with the JNI-mangled name
+  Java_de_hpi_collaborativefilteringkafka_nativeals_AlsNative_<method>, whose return and parameter types are the
+  JNI types of the Java signature (after JNIEnv*, jclass); every C ABI function the shim calls is declared in the
+  headers, exported by the library, and called with the header's argument count;
+- the re-plumbed MFeatureCalculator / UFeatureCalculator keep the reference's stores, sinks, last-iteration rule
+  and dependent-id filter (processors/MFeatureCalculator.java:32-34, :106-132; UFeatureCalculator.java:106-132),
+  take their GPU from TaskId.partition (not ProcessorContext.partition() in init), share one engine per (task,
+  side), and call the hot path once per half; NativeALSApp wires them into the reference's topology
+  (ALSApp.java:52-184) with the same node, store and topic names.
 """
 from __future__ import annotations
 
@@ -20,6 +30,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 JAVA = os.path.join(ROOT, "integration", "java", "de", "hpi", "collaborativefilteringkafka")
 FFM = os.path.join(JAVA, "nativeals", "AlsFfm.java")
 PROC = os.path.join(JAVA, "processors", "NativeMFeatureCalculator.java")
+UPROC = os.path.join(JAVA, "processors", "NativeUFeatureCalculator.java")
+COLL = os.path.join(JAVA, "processors", "NativeFeatureCollector.java")
+APP = os.path.join(JAVA, "apps", "NativeALSApp.java")
+TASK = os.path.join(JAVA, "nativeals", "TaskEngine.java")
+JNI_JAVA = os.path.join(JAVA, "nativeals", "AlsNative.java")
+JNI_C = os.path.join(ROOT, "integration", "jni", "cfk_als_jni.c")
+JNI_PREFIX = "Java_de_hpi_collaborativefilteringkafka_nativeals_AlsNative_"
+JNI_TYPES = {"int": "jint", "long": "jlong", "float": "jfloat", "void": "void", "short": "jshort",
+             "int[]": "jintArray", "long[]": "jlongArray", "float[]": "jfloatArray", "short[]": "jshortArray",
+             "byte[]": "jbyteArray", "String": "jstring"}
 
 
 def _ffm_layout(ct) -> str:
@@ -106,20 +126,126 @@ def test_invoke_exact_arity_matches_descriptors():
         assert n_args == len(desc[handles[h]]) - 1, f"{h}: {n_args} arguments, descriptor {desc[handles[h]]}"
 
 
-def test_replumbed_processor_keeps_the_reference_contract():
-    src = open(PROC).read()
+def _strip(src: str) -> str:
+    src = re.sub(r'"(\\.|[^"\\])*"', '""', src)
+    return re.sub(r"//[^\n]*|/\*.*?\*/", "", src, flags=re.S)
+
+
+def _split_params(params: str) -> list[str]:
+    params = " ".join(params.split())
+    return [p.strip() for p in params.split(",")] if params.strip() else []
+
+
+def _java_natives() -> dict[str, tuple[str, list[str]]]:
+    src = _strip(open(JNI_JAVA).read())
+    out = {}
+    for m in re.finditer(r"public\s+static\s+native\s+([\w\[\]]+)\s+(\w+)\s*\(([^)]*)\)\s*;", src):
+        ret, name, params = m.groups()
+        types = [p.rsplit(" ", 1)[0].strip() for p in _split_params(params)]
+        assert name not in out, f"overloaded native {name}: JNI short names would collide"
+        out[name] = (ret, types)
+    return out
+
+
+def _c_jni_functions() -> dict[str, tuple[str, list[str]]]:
+    src = _strip(open(JNI_C).read())
+    out = {}
+    for m in re.finditer(r"JNIEXPORT\s+(\w+)\s+JNICALL\s+(\w+)\s*\(([^)]*)\)\s*\{", src):
+        ret, name, params = m.groups()
+        types = [re.sub(r"\s*\w+$", "", p).replace(" ", "") for p in _split_params(params)]
+        out[name] = (ret, types)
+    return out
+
+
+def test_jni_shim_implements_every_native_method():
+    natives = _java_natives()
+    cfuns = _c_jni_functions()
+    assert len(natives) >= 14, natives.keys()
+    assert set(cfuns) == {JNI_PREFIX + n for n in natives}, (sorted(cfuns), sorted(natives))
+    for name, (ret, types) in natives.items():
+        assert "_" not in name, f"{name}: an underscore would need JNI escaping (_1)"
+        cret, ctypes_ = cfuns[JNI_PREFIX + name]
+        assert cret == JNI_TYPES[ret], (name, cret, ret)
+        assert ctypes_[:2] == ["JNIEnv*", "jclass"], (name, ctypes_)        # static natives
+        assert ctypes_[2:] == [JNI_TYPES[t] for t in types], (name, ctypes_, types)
+
+
+def _c_calls(src: str, name: str) -> list[int]:
+    """argument counts of every call of `name` in C source"""
+    counts = []
+    for m in re.finditer(rf"\b{name}\s*\(", src):
+        i, depth, n = m.end(), 1, 0
+        start = i
+        while depth:
+            ch = src[i]
+            if ch in "([{":
+                depth += 1
+            elif ch in ")]}":
+                depth -= 1
+            elif ch == "," and depth == 1:
+                n += 1
+            i += 1
+        counts.append(n + 1 if src[start:i - 1].strip() else 0)
+    return counts
+
+
+def test_jni_shim_calls_the_declared_c_abi():
+    headers = open(os.path.join(ROOT, "include", "als.h")).read() + open(
+        os.path.join(ROOT, "include", "als_host.h")).read()
+    src = _strip(open(JNI_C).read())
+    sigs, _ = _signatures()
+    called = sorted(set(re.findall(r"\b(als_\w+)\s*\(", src)))
+    assert "als_solve_half" in called and "als_set_block_coo" in called and "als_predict" in called
+    for name in called:
+        assert re.search(rf"\b{name}\s*\(", headers), f"{name} not declared in include/*.h"
+        assert name in sigs, f"{name} is not a library export"
+        for n in _c_calls(src, name):
+            assert n == len(sigs[name][1]), f"{name} called with {n} arguments, prototype has {len(sigs[name][1])}"
+
+
+def test_native_processors_keep_the_reference_contract():
+    m, u = _strip(open(PROC).read()), _strip(open(UPROC).read())
     for store in ("M_INBLOCKS_UID_STORE", "M_INBLOCKS_RATINGS_STORE", "M_OUTBLOCKS_STORE"):
-        assert f"ALSApp.{store}" in src
-    assert src.count("AlsFfm.solveHalf(") == 1          # one hot-path call per half, no per-entity solve
-    assert "CommonOps_FDRM" not in src and "org.ejml" not in src
-    assert "MOVIE_FEATURES_SINK + ALSApp.NUM_ALS_ITERATIONS" in src          # final-iteration sink (:117-123)
-    assert "(id % ALSApp.NUM_PARTITIONS) == targetPartition" in src          # out-block filter (:126)
-    assert "AlsFfm.setBlockCoo(" in src and "AlsFfm.readFactors(" in src
+        assert f"ALSApp.{store}" in m
+    for store in ("U_INBLOCKS_MID_STORE", "U_INBLOCKS_RATINGS_STORE", "U_OUTBLOCKS_STORE"):
+        assert f"ALSApp.{store}" in u
+    for src in (m, u):
+        assert src.count("engine.solve(") == 1          # one hot-path call per half, no per-entity solve
+        assert "CommonOps_FDRM" not in src and "org.ejml" not in src
+        assert "(id % ALSApp.NUM_PARTITIONS) == targetPartition" in src      # out-block filter (:125-126)
+        assert "TaskEngine.acquire(context.taskId()," in src                 # engine shared per (task, side)
+        assert "context.partition()" not in src                              # invalid outside process()
+        assert "engine.release()" in src
+    assert "MOVIE_FEATURES_SINK + ALSApp.NUM_ALS_ITERATIONS" in m            # M_{N-1} to the collector (:117-123)
+    assert "MOVIE_FEATURES_SINK + iteration" in m
+    # UFeatureCalculator.java:106-131: sink iteration i + 1; the last iteration goes to the collector ONLY
+    assert "sinkTopicIteration = sourceTopicIteration + 1" in u
+    last = u.index("if (sourceTopicIteration == ALSApp.NUM_ALS_ITERATIONS - 1)")
+    assert u.index("} else {", last) < u.index("uOutBlocksStore.get(userId)", last)
+    task = _strip(open(TASK).read())
+    assert task.count("AlsNative.solveHalf(") == 1 and "AlsNative.setBlockCoo(" in task
+    assert "task.partition" in task and "REGISTRY" in task                  # one engine per (task, side)
 
 
-@pytest.mark.parametrize("path", [FFM, PROC])
+def test_native_topology_mirrors_the_reference():
+    raw = open(APP).read()
+    app = _strip(raw)
+    assert "extends ALSApp" in app
+    for proc in ("NativeMFeatureCalculator::new", "NativeUFeatureCalculator::new", "NativeFeatureCollector::new",
+                 "MRatings2BlocksProcessor::new", "URatings2BlocksProcessor::new", "UFeatureInitializer::new"):
+        assert proc in app, proc
+    assert "MFeatureCalculator::new" not in app.replace("NativeMFeatureCalculator::new", "")
+    for name in ('"MFeatureCalculator-" + i', '"UFeatureCalculator-" + i', '"FeatureCollector"',
+                 '"user-features-source-" + i', '"movie-features-source-" + i', "MOVIE_FEATURES_SINK + NUM_ALS_ITERATIONS",
+                 "USER_FEATURES_SINK + (i + 1)", '"movie-features-final-source"', '"user-features-final-source"'):
+        assert name in raw, name
+    coll = _strip(open(COLL).read())
+    assert "AlsNative.predict(" in coll and "AlsNative.writePredictionMatrixCsv(" in coll
+    assert '"./predictions/prediction_matrix_"' in open(COLL).read()
+
+
+@pytest.mark.parametrize("path", [FFM, PROC, UPROC, COLL, APP, TASK, JNI_JAVA, JNI_C])
 def test_java_sources_are_balanced(path):
-    src = re.sub(r'"(\\.|[^"\\])*"', '""', open(path).read())
-    src = re.sub(r"//[^\n]*|/\*.*?\*/", "", src, flags=re.S)
+    src = _strip(open(path).read())
     for o, c in ("()", "{}", "[]"):
         assert src.count(o) == src.count(c), f"{os.path.basename(path)}: unbalanced {o}{c}"

@@ -1,0 +1,118 @@
+"""Guard on the shipped gfx950 code object (CPU only): the fix of the round-1 wrong-row hazard must survive
+rebuilds and compiler changes.
+
+The hazard: packed-fp32 VALU (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32) scheduled beside
+in-flight v_mfma_f32_16x16x32_bf16 intermittently lost a partial RHS on gfx950. The fix has two parts, both
+checked here on the code object inside libcfk_als.so (extracted with clang-offload-bundler, disassembled with
+llvm-objdump --mcpu=gfx950):
+  1. the kernels are built with -fno-slp-vectorize (csrc/Makefile): no v_pk_{add,mul,fma}_f32 in any als_solve_*
+     kernel;
+  2. every split-Gram MFMA group ends with MFMA_DRAIN (two `s_nop 7`, als_kernels.hip): after each
+     v_mfma_f32_16x16x32_bf16, no instruction writes its SrcA or SrcB registers -- which LLVM models as read at
+     issue -- before that drain, and no branch leaves before it. SrcC, when it is not the MFMA's own destination
+     (an accumulator the register allocator moves, KP = 128), is not checked: the compiler's hazard recognizer
+     models that WAR and pads it itself (e.g. `s_nop 4` before the v_accvgpr_write of a source accumulator).
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+LIB = os.path.join(ROOT, "collaborative-filtering-kafka_amd", "build", "libcfk_als.so")
+REG = re.compile(r"([va])\[(\d+):(\d+)\]|([va])(\d+)\b")
+
+
+def _regs(op):
+    m = REG.fullmatch(op.strip())
+    if not m:
+        return set()
+    if m.group(1):
+        return {(m.group(1), i) for i in range(int(m.group(2)), int(m.group(3)) + 1)}
+    return {(m.group(4), int(m.group(5)))}
+
+
+@pytest.fixture(scope="module")
+def kernels(tmp_path_factory):
+    if not os.path.exists(LIB):
+        pytest.fail(f"{LIB} not built (run __graft_entry__.build())")
+    d = tmp_path_factory.mktemp("isa")
+    fat, co = str(d / "fat.bin"), str(d / "co.elf")
+    subprocess.run([f"{LLVM}/llvm-objcopy", "--dump-section", f".hip_fatbin={fat}", LIB, str(d / "lib.so")],
+                   check=True)
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}", f"--output={co}"], check=True)
+    asm = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", co], check=True, capture_output=True,
+                         text=True).stdout
+    out, name = {}, None
+    for line in asm.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(\S+)>:$", line)
+        if m:
+            name = m.group(1)
+            out[name] = []
+            continue
+        t = line.strip()
+        if name is None or not t or t.startswith(("<", ";")):
+            continue
+        code = t.split("//")[0].strip()
+        if not code:
+            continue
+        op, _, rest = code.partition(" ")
+        out[name].append((op, [o.strip() for o in rest.split(",")] if rest.strip() else []))
+    return out
+
+
+def _solve_kernels(kernels):
+    ks = {n: ins for n, ins in kernels.items() if "als_solve_" in n}
+    assert len(ks) >= 12, sorted(kernels)
+    return ks
+
+
+def test_no_packed_fp32_valu_in_solve_kernels(kernels):
+    bad = {n: sorted({op for op, _ in ins if re.fullmatch(r"v_pk_(add|mul|fma)_f32", op)})
+           for n, ins in _solve_kernels(kernels).items()}
+    bad = {n: ops for n, ops in bad.items() if ops}
+    assert not bad, f"packed fp32 VALU in solve kernels (build without -fno-slp-vectorize?): {bad}"
+
+
+def _writes(op, ops):
+    if not ops:
+        return set()
+    if op.startswith("v_") or op.startswith("ds_read") or re.match(r"(global|buffer|flat|scratch)_load", op):
+        if "_lds" in op:                       # LDS-DMA: no VGPR destination
+            return set()
+        return _regs(ops[0])
+    return set()
+
+
+def test_every_split_gram_mfma_is_drained_before_its_operands_change(kernels):
+    checked, violations = 0, []
+    for name, ins in _solve_kernels(kernels).items():
+        for i, (op, ops) in enumerate(ins):
+            if op != "v_mfma_f32_16x16x32_bf16":
+                continue
+            checked += 1
+            dst = _regs(ops[0])
+            srcs = _regs(ops[1]) | _regs(ops[2])
+            drained, ws = False, 0
+            for j in range(i + 1, len(ins)):
+                op2, ops2 = ins[j]
+                if op2 == "s_nop" and ops2 and ops2[0] == "7" and j + 1 < len(ins) and ins[j + 1] == ("s_nop", ["7"]):
+                    drained = True
+                    break
+                if op2.startswith(("s_branch", "s_cbranch", "s_setpc", "s_endpgm")):
+                    break
+                ws += int(ops2[0], 0) + 1 if op2 == "s_nop" else 1
+                if op2.startswith("v_mfma"):
+                    continue
+                w = _writes(op2, ops2)
+                if w & srcs:
+                    violations.append((name, i, op2, " ".join(ops2[:2]), ws))
+                    break
+            if not drained and not (violations and violations[-1][1] == i):
+                violations.append((name, i, "no MFMA_DRAIN before a branch / the end", ""))
+    assert checked > 100, checked
+    assert not violations, violations[:8]

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """A/B kernel variants in ONE process with interleaved rounds (cdna_hip_programming.md §5.4 rule 24).
 
-  python tools/kbench.py --variants "ALS_MFMA_WAVES=2" "ALS_MFMA_WAVES=3" [--rounds 5] [--nnz ...]
+  python tools/kbench.py --variants "ALS_DUAL=1" "ALS_DUAL=0" [--rounds 5] [--nnz ...]
+  CFK_ALS_LIB=collaborative-filtering-kafka_amd/build_debug/libcfk_als.so python tools/kbench.py \
+      --variants "ALS_DEBUG_SKIP_SOLVE=0" "ALS_DEBUG_SKIP_SOLVE=1"   # Gram / solve split: debug build only
 
 Each variant is a set of env settings read at engine creation / block upload. Prints per-variant median and
 min device time (HIP events) of the main + reduce launches of each half on the Netflix-shape workload.
@@ -21,7 +23,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", nargs="+", default=["ALS_MFMA_WAVES=2"])
+    ap.add_argument("--variants", nargs="+", default=["ALS_DUAL=1"])
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--k", type=int, default=64)
     ap.add_argument("--users", type=int, default=480_189)

@@ -9,7 +9,9 @@ Writes:
                               KiB -> B, FETCH doubled on gfx950), and the SQ counters of the full launch and of
                               the Gram alone (ALS_DEBUG_SKIP_SOLVE=1): MFMA busy share, issue stalls, clock
   bench_line.json             the bench.py line of the same call
-and profiles/traffic.json (k = 64) or traffic_k<k>.json (read by bench.py: per_side HBM bytes per launch).
+and profiles/counters_k<k>.json (read by bench.py): per side the HBM bytes per launch, the MFMA-pipe busy share of
+the whole launch and of the Gram alone (debug build, ALS_DEBUG_SKIP_SOLVE=1), the sustained clock, and the solve
+phase = whole launch minus Gram-only counters (its share of the launch's cycles, MFMA busy and VALU issue share).
 Sides: the main solve kernel dispatch with the largest grid is the user half (480,189 tasks), the next the movie
 half (FULL + PARTIAL tasks); the REDUCE kernel instantiation is recognised by its last template argument.
 
@@ -120,13 +122,37 @@ def main(tag, name):
     bench = json.loads(open(os.path.join(dst, "bench_line.json")).read()) if os.path.exists(os.path.join(dst, "bench_line.json")) else {}
     cfg = bench.get("config", {})
     k = cfg.get("k", 64)
-    tname = "traffic.json" if k == 64 else f"traffic_k{k}.json"
-    json.dump({"k": k, "nnz": cfg.get("nnz", 100_000_000),
-               "per_side": {s: traffic[s]["hbm_bytes"] for s in ("movie", "user") if s in traffic},
-               "detail": traffic, "source": f"profiles/{name}",
-               "note": "per launch: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> B; Infinity-Cache hits "
-                       "are counted by these counters"}, open(os.path.join(ROOT, "profiles", tname), "w"),
-              indent=1)
+    SIMDS, XCDS = 1024, 8
+    per_side = {}
+    for side in ("movie", "user"):
+        sq, gr = out.get("sq", {}).get(side), out.get("sq_gram", {}).get(side)
+        tr_ms = out["trace"].get(side, {}).get("avg_ms_without_first")
+        d = {"hbm_bytes": traffic.get(side, {}).get("hbm_bytes"), "trace_avg_ms": tr_ms}
+        if sq:
+            cyc = sq["GRBM_GUI_ACTIVE"] / XCDS                   # GPU cycles of the launch (summed over XCDs)
+            d["mfma_busy_frac"] = sq["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * SIMDS)
+            d["valu_issue_frac"] = sq["SQ_INSTS_VALU"] / (cyc * SIMDS)
+            d["wait_inst_any_frac"] = sq["SQ_WAIT_INST_ANY"] / sq["SQ_WAVE_CYCLES"]
+            if tr_ms:
+                d["clock_ghz"] = cyc / (tr_ms * 1e-3) / 1e9
+            if gr:
+                gcyc = gr["GRBM_GUI_ACTIVE"] / XCDS
+                d["gram_only"] = {"cycles_frac": gcyc / cyc,
+                                  "mfma_busy_frac": gr["SQ_VALU_MFMA_BUSY_CYCLES"] / (gcyc * SIMDS),
+                                  "valu_issue_frac": gr["SQ_INSTS_VALU"] / (gcyc * SIMDS)}
+                scyc = cyc - gcyc
+                if scyc > 0:
+                    d["solve_phase"] = {
+                        "cycles_frac": scyc / cyc,
+                        "mfma_busy_frac": (sq["SQ_VALU_MFMA_BUSY_CYCLES"] - gr["SQ_VALU_MFMA_BUSY_CYCLES"]) / (scyc * SIMDS),
+                        "valu_issue_frac": (sq["SQ_INSTS_VALU"] - gr["SQ_INSTS_VALU"]) / (scyc * SIMDS),
+                        "note": "whole launch minus the Gram-only launch of the same blocks (debug build)"}
+        per_side[side] = d
+    json.dump({"k": k, "nnz": cfg.get("nnz", 100_000_000), "per_side": per_side, "source": f"profiles/{name}",
+               "note": "per launch; hbm_bytes = FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> B (Infinity-Cache "
+                       "hits are counted by these counters); *_frac over 1024 SIMDs x the launch's GPU cycles "
+                       "(GRBM_GUI_ACTIVE / 8 XCDs)"},
+              open(os.path.join(ROOT, "profiles", f"counters_k{k}.json"), "w"), indent=1)
     print(json.dumps({k: out[k] for k in ("trace", "traffic")}, indent=1))
 
 
