@@ -106,9 +106,9 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
 // Short rows in entry space (als_solve_dual): fp32 split path, kp 64 with cd 2, kp 128 with cd 2 or 4 (rows of
 // 16 * cd padded entries, i.e. cd / 2 blocks); `a.tasks` are FULL tasks of such rows.
 hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s);
-// Pre-split of an fp32 [n_rows][64] factor table (sentinel row included) into the bf16 h/m/l piece layout
-// the presplit Gram gathers: row r, lane piece j (features 4j..4j+3) = 6 dwords at byte r*384 + j*24:
-// h(f0,f1) h(f2,f3) m(f0,f1) m(f2,f3) l(f0,f1) l(f2,f3).
+// Pre-split of an fp32 [n_rows][64] factor table (sentinel row included) into the bf16 h/m/l pieces the
+// presplit Gram gathers: row r = 384 B at r*384 = [h, m of the 16 lane pieces: 16 x 16 B][l of the 16 pieces:
+// 16 x 8 B], lane piece j = features 4j..4j+3.
 constexpr int PRESPLIT_ROW_BYTES = 384;
 hipError_t launch_presplit(const float* src, void* dst, int64_t n_rows, hipStream_t s);
 // padded fp32 ratings -> bf16 pairs (n_pairs = nnz_padded / 2)
