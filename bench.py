@@ -37,8 +37,11 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFS = 157.3        # f32 vector = f32 MFMA dense peak
 BF16_MFMA_PEAK_TFS = 2500.0  # dense bf16 MFMA peak (no sparsity)
 # MI355X_MICROARCH.md "Indexed rows: gather into LDS": uniformly random rows of a 151 MB table (the 123 MB k = 64
-# user table the movie half gathers sits between its 38 MB and 151 MB rows) are served at 7.4-7.9 TB/s chip-wide
+# user table the movie half gathers sits between its 38 MB and 151 MB rows) are served at 7.4-7.9 TB/s chip-wide;
+# rows every workgroup shares from the XCD's L2 (the 6.8 MB pre-split movie table of the user half: 91% L2 hits)
+# at 16.8-18.8 TB/s
 IC_GATHER_CEILING_GBS = 7900.0
+L2_GATHER_CEILING_GBS = 18800.0
 MFMA_BF16_FLOP = 16 * 16 * 32 * 2   # one v_mfma_f32_16x16x32_bf16
 
 
@@ -242,11 +245,19 @@ def main():
             mf = ((main_blocks * mfma_per_block(kp, path["presplit"]) + dual_mfma) * MFMA_BF16_FLOP
                   if path["gram_path"] == "mfma_split" else 0)
             c = (ctr or {}).get("per_side", {}).get(side, {})
-            gather_bound = kp <= 64 and not path["presplit"]
+            # bytes the launch requests from the memory hierarchy: the gathered opposite rows (pre-split: 384 B of
+            # bf16 h/m/l pieces per padded entry; fp32 otherwise, also for the entry-space rows), column indices,
+            # ratings (bf16 pairs on the pre-split path) and the written factor rows
+            dual_entries = sum(32 * (c_ + 1) * n for c_, n in enumerate(dual))
+            main_entries = main_blocks * 32
+            row_b = 384 if path["presplit"] else 4 * kp
+            gathered = (main_entries * (row_b + 4 + (2 if path["presplit"] else 4)) + dual_entries * (4 * kp + 8)
+                        + 4 * kp * i["n_rows"])
             d = {
                 "kernel": f"als_solve_mfma<{kp},{1 if kp == 128 else (3 if path['presplit'] else 2)},split,"
                           f"{'presplit' if path['presplit'] else 'on-the-fly split'}> + als_solve_dual (short rows)",
                 "avg_launch_ms": g_ms[side], "reduce_launch_ms": r_ms[side],
+                "gathered_bytes": gathered,
                 "mfma_bf16": {"per_32_entry_block": mfma_per_block(kp, path["presplit"]),
                               "flop_per_launch": mf, "executed_tflops": mf / t_s / 1e12, "peak": BF16_MFMA_PEAK_TFS,
                               "frac": mf / t_s / 1e12 / BF16_MFMA_PEAK_TFS},
@@ -260,35 +271,49 @@ def main():
             if c:
                 d["counters"] = c
                 d["traffic"] = c.get("hbm_bytes")
-            if gather_bound:
-                # the fabric gather of the opposite factor rows (L2 misses served by the Infinity Cache / HBM)
+            if kp <= 64 and not path["presplit"]:
+                # the fabric gather of the opposite factor rows: L2 misses served by the Infinity Cache / HBM
                 fab = c.get("hbm_bytes")
-                d.update(bound="gather", unit="GB/s", peak=IC_GATHER_CEILING_GBS,
+                d.update(bound="gather (Infinity Cache)", unit="GB/s", peak=IC_GATHER_CEILING_GBS,
                          achieved=(fab / t_s / 1e9) if fab else None,
                          limit="fabric gather of the opposite factor rows: PMC FETCH x2 + WRITE bytes / launch time "
                                "against the Infinity-Cache random-row gather ceiling (MI355X_MICROARCH.md)")
+            elif path["presplit"]:
+                # gathers served by L2 (the pre-split table is L2-resident): requested bytes against the L2 gather
+                # ceiling; the Gram phase alone (its cycle share from the counters) runs closer to it
+                d.update(bound="gather (L2)", unit="GB/s", peak=L2_GATHER_CEILING_GBS, achieved=gathered / t_s / 1e9,
+                         limit="L2 -> CU gather of the pre-split opposite rows (384 B per entry) in the Gram phase; "
+                               "the solve phase (counters.solve_phase) is latency-bound")
+                gf = c.get("gram_only", {}).get("cycles_frac")
+                if gf:
+                    d["gram_phase"] = {"achieved_gbs": gathered / (t_s * gf) / 1e9,
+                                       "frac": gathered / (t_s * gf) / 1e9 / L2_GATHER_CEILING_GBS}
             else:
                 d.update(bound="mfma", unit="TFLOP/s", peak=BF16_MFMA_PEAK_TFS, achieved=mf / t_s / 1e12,
-                         limit="MFMA pipe: the split-bf16 Gram's v_mfma_f32_16x16x32_bf16 flops as issued against "
-                               "the dense bf16 peak; counters.mfma_busy_frac = pipe-busy share of the launch")
+                         limit="MFMA pipe at one wave per SIMD: the split-bf16 Gram's v_mfma_f32_16x16x32_bf16 flops "
+                               "as issued against the dense bf16 peak; counters.mfma_busy_frac = pipe-busy share")
             d["frac"] = d["achieved"] / d["peak"] if d.get("achieved") else None
             per[side] = d
         dom = max(per, key=lambda s: per[s]["avg_launch_ms"])
         d = per[dom]
         roofline = {
-            "bound": d["bound"] if d["bound"] == "mfma" else "hbm", "achieved": d["achieved"], "peak": d["peak"],
+            "bound": "mfma" if d["bound"] == "mfma" else "hbm", "limiter": d["bound"],
+            "achieved": d["achieved"], "peak": d["peak"],
             "unit": d["unit"], "frac": d["frac"], "traffic": d.get("traffic"),
             "kernel": d["kernel"] + f" ({dom} half, the dominant launch)", "limit": d["limit"],
-            "avg_launch_ms": d["avg_launch_ms"], "counters": d.get("counters"),
+            "avg_launch_ms": d["avg_launch_ms"], "counters": d.get("counters"), "gram_phase": d.get("gram_phase"),
             "algorithmic_bytes_frac": d["algorithmic_bytes"]["frac_of_hbm"],
             "both_halves_algorithmic_gbs": (per["movie"]["algorithmic_bytes"]["bytes"] +
                                             per["user"]["algorithmic_bytes"]["bytes"])
                                            / ((g_ms["movie"] + g_ms["user"]) / 1000.0) / 1e9,
             "per_launch": per,
             "counters_source": (ctr or {}).get("source"),
-            "note": "achieved/frac: the dominant launch against its binding ceiling (bound); traffic = PMC FETCH_SIZE "
-                    "x2 + WRITE_SIZE per launch; counters = rocprofv3 SQ passes of this build (whole launch, Gram only, "
-                    "and their difference = the solve phase)",
+            "note": "achieved/frac: the dominant launch against its binding ceiling (limiter; bound = its memory "
+                    "(hbm) or compute (mfma) side): the gathered bytes it requests / launch time against the chip's "
+                    "gather ceiling for where those rows are served from (MI355X_MICROARCH.md), or executed MFMA "
+                    "flops against the dense bf16 peak; traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per launch (HBM / "
+                    "Infinity Cache side); counters = rocprofv3 SQ passes of this build (whole launch, Gram only, and "
+                    "their difference = the solve phase)",
         }
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
