@@ -46,6 +46,7 @@ struct Block {
     int32_t* d_col = nullptr;
     float* d_rat = nullptr;
     uint32_t* d_rat_pk = nullptr;   // pre-split blocks: ratings as bf16 pairs (the Gram's RHS operand)
+    int32_t* d_col_ps = nullptr;    // pre-split blocks: column indices in the LDS-DMA gather order
     Task* d_tasks = nullptr;        // FULL + PARTIAL, sorted by work (longest first)
     Task* d_reduce = nullptr;       // REDUCE
     int32_t n_tasks = 0, n_reduce = 0, n_slots = 0;
@@ -176,6 +177,7 @@ void free_block(Block& b) {
     (void)hipFree(b.d_col);
     (void)hipFree(b.d_rat);
     (void)hipFree(b.d_rat_pk);
+    (void)hipFree(b.d_col_ps);
     (void)hipFree(b.d_tasks);
     (void)hipFree(b.d_reduce);
     (void)hipFree(b.d_task_se);
@@ -508,6 +510,9 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
             if (st != hipSuccess) return fail(ALS_ERR_OUT_OF_MEMORY, "hipMalloc(%lld): %s", (long long)nnz_padded * 2,
                                               hipGetErrorString(st));
             st = cfk::launch_pack_ratings(blk.d_rat, blk.d_rat_pk, nnz_padded / 2, nullptr);
+            // and the column indices in the order of the LDS-DMA gather (one 16-B load per loader row)
+            if (st == hipSuccess) st = hipMalloc((void**)&blk.d_col_ps, (size_t)nnz_padded * 4);
+            if (st == hipSuccess) st = cfk::launch_pack_cols_ps(blk.d_col, blk.d_col_ps, nnz_padded, nullptr);
             if (st == hipSuccess) st = hipDeviceSynchronize();
             if (st != hipSuccess) return fail(ALS_ERR_DEVICE, "pack ratings: %s", hipGetErrorString(st));
         }
@@ -806,6 +811,7 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
             HIP_TRY(cfk::launch_presplit((const float*)opp.ptr, e->d_split, b.n_opp_rows + 1, e->stream));
         a.opp_split = e->d_split;
         a.rat_pk = b.d_rat_pk;
+        a.col_ps = b.d_col_ps;
     }
     HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves, b.presplit, false));
     if (side_dual) HIP_TRY(hipStreamWaitEvent(e->side_stream, e->fork, 0));

@@ -60,6 +60,8 @@ struct SolveArgs {
     uint32_t* integrity;    // device record of partial slots that failed their check (see als_kernels.hip)
     float refine_min_pivot; // MFMA tile solve: skip the refinement step when every scaled pivot >= this (> 1: never)
     const uint32_t* rat_pk; // presplit: the padded ratings as bf16 pairs (entries 2i, 2i+1), exact for |r| <= 256
+    const int32_t* col_ps;  // presplit: the padded column indices permuted per block for the LDS-DMA gather
+                            //   (launch_pack_cols_ps: lane group r of a block loads its 4 rows with one 16-B load)
     int32_t rows_per_chunk; // chunk-major slots (als_set_row_layout): 0 = factor row row_offset + row, else
     int64_t chunk_stride;   //   row_offset + (row / rows_per_chunk) * chunk_stride + row % rows_per_chunk
 };
@@ -106,11 +108,14 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
 // Short rows in entry space (als_solve_dual): fp32 split path, kp 64 with cd 2, kp 128 with cd 2 or 4 (rows of
 // 16 * cd padded entries, i.e. cd / 2 blocks); `a.tasks` are FULL tasks of such rows.
 hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s);
-// Pre-split of an fp32 [n_rows][64] factor table (sentinel row included) into the bf16 h/m/l pieces the
-// presplit Gram gathers: row r = 384 B at r*384 = [h, m of the 16 lane pieces: 16 x 16 B][l of the 16 pieces:
-// 16 x 8 B], lane piece j = features 4j..4j+3.
+// Pre-split of an fp32 [n_rows][64] factor table (sentinel row included) into the bf16 h/m/l terms the
+// presplit Gram stages in LDS: row r = 384 B at r*384 = three 128-B planes (h, m, l), plane position
+// 16 b + j (b = 0..3, j = 0..15) holding feature 4 j + b, so the 16 values one transposed LDS read hands to a
+// 16-lane group (features 4 j + b, j = 0..15) are 32 contiguous bytes.
 constexpr int PRESPLIT_ROW_BYTES = 384;
 hipError_t launch_presplit(const float* src, void* dst, int64_t n_rows, hipStream_t s);
+// padded column indices -> the per-block order of the presplit gather (n_entries = nnz_padded)
+hipError_t launch_pack_cols_ps(const int32_t* col, int32_t* dst, int64_t n_entries, hipStream_t s);
 // padded fp32 ratings -> bf16 pairs (n_pairs = nnz_padded / 2)
 hipError_t launch_pack_ratings(const float* rat, uint32_t* dst, int64_t n_pairs, hipStream_t s);
 // bytes % 16 == 0; host_pinned must stay valid until the stream has passed the copy

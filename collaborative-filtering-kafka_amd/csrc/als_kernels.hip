@@ -830,17 +830,50 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 template <int KP>
 constexpr int mfma_waves() { return WAVES; }
 
-// Pre-split row layout: [h,m pieces][l pieces] (1: contiguous gathers for a 16-lane group) or [h,m,l] per 24-B
-// piece (0).
-#ifndef CFK_PRESPLIT_HML
-#define CFK_PRESPLIT_HML 1
+// Pre-split Gram with an LDS image (1): the gathered h/m/l rows go straight to LDS by LDS-DMA
+// (global_load_lds_dwordx4) and the MFMA operands come back with transposed reads (ds_read_b64_tr_b16), so no
+// VALU transposes and no gather registers; table layout: b-major planes (als_internal.h). 0: the register path
+// (v_perm_b32 transposes of gathered [h,m | l] pieces), kept as the A/B baseline.
+#ifndef CFK_PRESPLIT_LDS
+#define CFK_PRESPLIT_LDS 1
 #endif
-// Pre-split Gram: a block's 32 column indices and 32 ratings come with ONE 4-B load per lane (lane (g, j < 8):
-// column of entry 8g + j, lane (g, j >= 8): its rating) and reach the 16 lanes of group g by DPP row_newbcast (1),
-// instead of four 16-B loads per lane that every lane of a group issues for the same 8 entries (0).
-#ifndef CFK_PRESPLIT_CR
-#define CFK_PRESPLIT_CR 1
-#endif
+#if CFK_PRESPLIT_LDS
+// fp32 table -> bf16 h/m/l planes (PRESPLIT_ROW_BYTES per row): thread (row, b, jh) splits features
+// 4 (8 jh + i) + b, i = 0..7, and writes 16 B per plane at position 16 b + 8 jh.
+__global__ __launch_bounds__(256) void als_presplit(const float* __restrict__ src, unsigned* __restrict__ dst,
+                                                   int64_t n_threads) {
+    constexpr int C = 4, KP = 64;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= n_threads) return;
+    const int64_t row = t / (2 * C);
+    const int b = (int)(t % (2 * C)) >> 1, jh = (int)(t & 1);
+    const float* s = src + row * KP + C * 8 * jh + b;
+    u32x4 h, m, l;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        unsigned hh, mm, ll;
+        split3(s[C * (2 * i)], s[C * (2 * i + 1)], hh, mm, ll);
+        h[i] = hh;
+        m[i] = mm;
+        l[i] = ll;
+    }
+    unsigned* o = dst + row * (PRESPLIT_ROW_BYTES / 4) + (16 * b + 8 * jh) / 2;
+    *(u32x4*)o = h;
+    *(u32x4*)(o + 2 * KP / 4) = m;
+    *(u32x4*)(o + 4 * KP / 4) = l;
+}
+// In-block column indices in the order of the LDS-DMA gather: inside a 32-entry block, word 4 r + x (r = 0..7,
+// x = 0..3) holds the column of entry k = 16 (x >> 1) + 8 (r >> 2) + 4 (x & 1) + (r & 3), so the 8 lanes of loader
+// row r fetch the rows of their 4 DMA instructions with one 16-B load.
+__global__ __launch_bounds__(256) void als_pack_cols_ps(const int32_t* __restrict__ col, int32_t* __restrict__ dst,
+                                                       int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int w = (int)(i & 31), r = w >> 2, x = w & 3;
+    const int k = 16 * (x >> 1) + 8 * (r >> 2) + 4 * (x & 1) + (r & 3);
+    dst[i] = col[(i & ~(int64_t)31) + k];
+}
+#else
 // fp32 table -> bf16 h/m/l pieces (PRESPLIT_ROW_BYTES per row), one thread per 16-B row piece.
 __global__ __launch_bounds__(256) void als_presplit(const float* __restrict__ src, unsigned* __restrict__ dst,
                                                    int64_t n_pieces) {
@@ -850,20 +883,14 @@ __global__ __launch_bounds__(256) void als_presplit(const float* __restrict__ sr
     unsigned h01, m01, l01, h23, m23, l23;
     split3(x[0], x[1], h01, m01, l01);
     split3(x[2], x[3], h23, m23, l23);
-    if constexpr (CFK_PRESPLIT_HML) {
-        // row = [h, m of 16 pieces: 16 x 16 B][l of 16 pieces: 16 x 8 B], so both gathers of a 16-lane group
-        // are contiguous (16-B and 8-B lane strides)
-        unsigned* o = dst + (t >> 4) * (PRESPLIT_ROW_BYTES / 4);
-        const int j = (int)(t & 15);
-        *(u32x4*)(o + 4 * j) = u32x4{h01, h23, m01, m23};
-        *(u32x2*)(o + 64 + 2 * j) = u32x2{l01, l23};
-    } else {
-        unsigned* o = dst + t * 6;
-        *(u32x2*)o = u32x2{h01, h23};
-        *(u32x2*)(o + 2) = u32x2{m01, m23};
-        *(u32x2*)(o + 4) = u32x2{l01, l23};
-    }
+    // row = [h, m of 16 pieces: 16 x 16 B][l of 16 pieces: 16 x 8 B], so both gathers of a 16-lane group are
+    // contiguous (16-B and 8-B lane strides)
+    unsigned* o = dst + (t >> 4) * (PRESPLIT_ROW_BYTES / 4);
+    const int j = (int)(t & 15);
+    *(u32x4*)(o + 4 * j) = u32x4{h01, h23, m01, m23};
+    *(u32x2*)(o + 64 + 2 * j) = u32x2{l01, l23};
 }
+#endif
 
 // REDUCE = true: the launch of a half's REDUCE tasks (sum of partial slots + solve), compiled apart from the
 // gather kernel so neither carries the other's code and registers.
@@ -876,6 +903,10 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
     __shared__ __attribute__((aligned(16))) float sbuf[NW][KP];
     constexpr int TL = tile_lds_floats<C>();
     __shared__ __attribute__((aligned(16))) float tiles_lds[NW][TL > 0 ? TL : 1];
+    // pre-split Gram: one block's LDS image per wave (LDS-DMA target)
+    constexpr int STAGE = (PRESPLIT && !REDUCE && CFK_PRESPLIT_LDS) ? 3 * C * 1024 : 16;
+    __shared__ __attribute__((aligned(1024))) unsigned char stage_lds[NW][STAGE];
+    (void)stage_lds;
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tid = blockIdx.x * NW + wave;
@@ -964,98 +995,19 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             for (int c = 0; c < C; ++c) acc.rhs[c] += r * y[c];
         };
         if constexpr (PRESPLIT) {
-            // Split-bf16 Gram over a PRE-SPLIT opposite table (als_presplit, once per half): lane (g, j) loads
-            // the 24-B h/m/l piece of features 4j..4j+3 of its group's 8 entries and only transposes bf16
-            // halves into the MFMA operands (v_perm_b32: 48 per block instead of ~150 split instructions).
-            // The RHS Y^T r becomes 12 more MFMAs (B[k][*] = r_k, so every column of the result holds Y_b^T r;
-            // the engine picks this variant only for blocks whose ratings are exact in bf16, |r| <= 256). Chosen for tables that stay L2-resident (the 17,770-row
-            // movie table the user half reads): 1.5x the gathered bytes, far fewer VALU instructions.
+            // Split-bf16 Gram over a PRE-SPLIT opposite table (als_presplit, once per half: the h/m/l bf16 terms of
+            // every factor row). The RHS Y^T r is 12 more MFMAs (B[k][*] = r_k, so every column of the result holds
+            // Y_b^T r; the engine picks this variant only for blocks whose ratings are exact in bf16, |r| <= 256).
+            // Chosen for tables that stay L2-resident (the 17,770-row movie table the user half reads).
             static_assert(C == 4, "pre-split Gram: KP = 64");
             typedef int i32x4 __attribute__((ext_vector_type(4)));
-            struct Cols { i32x4 i[2]; };
-            struct Rats { f32x4 r[2]; };
-            struct Piece { unsigned w[6]; };
-            auto load_cols = [&](int blk, Cols& x) {
-                const int32_t* c = cb + (int64_t)blk * BLOCK_ENTRIES;
-                x.i[0] = *(const i32x4*)c;
-                x.i[1] = *(const i32x4*)(c + 4);
-            };
-            auto load_rats = [&](int blk, Rats& x) {
-                const float* r = rb + (int64_t)blk * BLOCK_ENTRIES;
-                x.r[0] = *(const f32x4*)r;
-                x.r[1] = *(const f32x4*)(r + 4);
-            };
-            const char* sbase = (const char*)a.opp_split + (CFK_PRESPLIT_HML ? j * 16 : j * 24);
             const char* tbase = (const char*)a.opp_split;
-            const uint32_t hm_off = 16u * j, l_off = 256u + 8u * j;
-            auto gather_blk = [&](const Cols& x, Piece (&y)[B]) {
-#pragma unroll
-                for (int t = 0; t < B; ++t) {
-                    // 24-bit multiply (full rate; pre-split tables are small: host-checked < 2^24 rows)
-                    const char* p = sbase + __umul24((uint32_t)x.i[t >> 2][t & 3], (uint32_t)PRESPLIT_ROW_BYTES);
-                    if constexpr (CFK_PRESPLIT_HML) {
-                        // wave-uniform table base + 32-bit per-lane offsets (saddr form: one 24-bit multiply-add per
-                        // load instead of a 64-bit address per lane); l piece j at 256 + 8 j
-                        const uint32_t ro = __umul24((uint32_t)x.i[t >> 2][t & 3], (uint32_t)PRESPLIT_ROW_BYTES);
-                        const u32x4 hm = *(const u32x4*)(tbase + (ro + hm_off));
-                        const u32x2 l = *(const u32x2*)(tbase + (ro + l_off));
-                        y[t].w[0] = hm[0]; y[t].w[1] = hm[1];
-                        y[t].w[2] = hm[2]; y[t].w[3] = hm[3];
-                        y[t].w[4] = l[0]; y[t].w[5] = l[1];
-                    } else {
-                        const u32x2 a0 = *(const u32x2*)p, a1 = *(const u32x2*)(p + 8), a2 = *(const u32x2*)(p + 16);
-                        y[t].w[0] = a0[0]; y[t].w[1] = a0[1];
-                        y[t].w[2] = a1[0]; y[t].w[3] = a1[1];
-                        y[t].w[4] = a2[0]; y[t].w[5] = a2[1];
-                    }
-                }
-            };
             f32x4 racc[C];
 #pragma unroll
             for (int b = 0; b < C; ++b) racc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-            // CFK_PRESPLIT_CR: one 4-B load per lane and block, expanded by DPP broadcasts inside the group
-            // lane (g, j < 8): column of entry 8g + j; lane (g, 8 + q): bf16 rating pair (8g + 2q, 8g + 2q + 1)
-            // (lanes 12..15 repeat pairs 0..3)
-            const int32_t* crb = j < 8 ? a.col + tk.begin + g * B + j
-                                       : (const int32_t*)a.rat_pk + (tk.begin >> 1) + g * 4 + (j & 3);
-            const int cshift = j < 8 ? 5 : 4;   // per-block stride: 32 columns or 16 rating pairs
-            auto load_cr = [&](int blk) { return crb[blk << cshift]; };
-            auto expand_cr = [&](int v, Cols& I, u32x4& R) {
-                static_for<0, 8>([&](auto T) {
-                    constexpr int t = T;
-                    I.i[t >> 2][t & 3] = __builtin_amdgcn_mov_dpp(v, 0x150 + t, 0xf, 0xf, false);
-                });
-                static_for<0, 4>([&](auto Q) {
-                    constexpr int q = Q;
-                    R[q] = (unsigned)__builtin_amdgcn_mov_dpp(v, 0x150 + 8 + q, 0xf, 0xf, false);
-                });
-            };
-            auto step = [&](const Piece (&y)[B], const auto& x) {
-                u32x4 P[3][C];   // plane (h, m, l) x feature block b: entries 0..7 as bf16 pairs
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-                    for (int b = 0; b < C; ++b)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            unsigned v = __builtin_amdgcn_perm(y[2 * q + 1].w[2 * pl + (b >> 1)],
-                                                               y[2 * q].w[2 * pl + (b >> 1)],
-                                                               (b & 1) ? 0x07060302u : 0x05040100u);
-                            pin(v);
-                            P[pl][b][q] = v;
-                        }
-                u32x4 R;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    unsigned v;
-                    if constexpr (std::is_same_v<std::decay_t<decltype(x)>, Rats>)
-                        v = pk_bf16(x.r[q >> 1][2 * (q & 1)], x.r[q >> 1][2 * (q & 1) + 1]);
-                    else
-                        v = x[q];   // packed by expand_cr
-                    pin(v);
-                    R[q] = v;
-                }
-                __builtin_amdgcn_sched_barrier(0);
+            // the block's MFMAs on operands P[plane h/m/l][feature block b] (entries 8g..8g+7 of feature 4j + b as
+            // bf16 pairs) and the bf16 rating pairs R of the same entries
+            auto mfma_block = [&](const u32x4 (&P)[3][C], const u32x4& R) {
 #pragma unroll
                 for (int b1 = 0; b1 < C; ++b1)
 #pragma unroll
@@ -1086,95 +1038,164 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                 }
                 MFMA_DRAIN();
             };
-            if constexpr (CFK_PRESPLIT_CR && MINW >= 3) {
-                // three waves per SIMD (168 VGPRs): one gather buffer, the other waves hide its latency; the
-                // block's columns/ratings are still loaded one block ahead
-                if (nblk > 0) {
-                    Cols I;
-                    u32x4 R;
-                    Piece Y[B];
-                    const int lastb = nblk - 1;
-                    int v = load_cr(0);
-                    for (int b = 0; b < nblk; ++b) {
-                        expand_cr(v, I, R);
-                        gather_blk(I, Y);
-                        v = load_cr(min(b + 1, lastb));
-                        __builtin_amdgcn_sched_barrier(0);
-                        step(Y, R);
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-                }
-            } else if constexpr (CFK_PRESPLIT_CR) {
-              if (nblk > 0) {
-                // same pipeline as below: loads two blocks ahead of their gathers' use, gathers one block ahead
-                Cols I;
-                u32x4 R0, R1;
-                Piece Y0[B], Y1[B];
+#if CFK_PRESPLIT_LDS
+            // LDS image of one 32-entry block per wave (12 KB): 12 LDS-DMA instructions (plane pl, entry quarter m)
+            // of 1 KB, instruction (pl, m) = 8 rows x one 128-B plane, lane 8 r + i holding 16-B chunk
+            // i ^ 2 (r >> 1) of the row of entry k = 16 (m >> 1) + 8 (r >> 2) + 4 (m & 1) + (r & 3): whole cache
+            // lines per row for the address unit (8 lines per instruction, as many as the register gathers), and a
+            // chunk swizzle that makes the transposed reads conflict-free. Operand (pl, b) of lane (g, 4 q + p) =
+            // two ds_read_b64_tr_b16 (h = 0, 1: entries 8 g + 4 h + 0..3), lane 4 q + p addressing entry
+            // 8 g + 4 h + q, plane positions 16 b + 4 p .. + 3 (features 4 j + b, j = 4 p .. 4 p + 3); the 16 lanes
+            // of a group receive features j = 0..15 of their 4 entries: exactly the registers the v_perm
+            // transposes built. Same products, same order: bitwise equal to the register path.
+            typedef short s16x4 __attribute__((ext_vector_type(4)));
+            typedef __attribute__((address_space(3))) void lds_void;
+            typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+            constexpr int IMG = 3 * 4 * 1024;
+            static_assert(sizeof(stage_lds[0]) >= IMG, "stage image");
+            unsigned char* img = stage_lds[uni(wave)];
+            const int r8 = lane >> 3;
+            const uint32_t ld_off = 16u * (uint32_t)((lane & 7) ^ (2 * (r8 >> 1)));
+            const int q = (lane >> 2) & 3, p = lane & 3, rr = 4 * (g & 1) + q;
+            uint32_t rd[C];
+#pragma unroll
+            for (int b = 0; b < C; ++b)
+                rd[b] = 2048u * (uint32_t)(g >> 1) + 16u * (uint32_t)(8 * rr + ((2 * b + (p >> 1)) ^ (2 * (rr >> 1)))) +
+                        8u * (uint32_t)(p & 1);
+            // per-plane table bases kept in SGPRs (opaque to the optimiser: folded into the per-lane offset they
+            // would force 64-bit addresses; an LDS-DMA takes no immediate offset here, it would move the LDS
+            // destination too), so every DMA takes the saddr form with one 32-bit lane offset per row
+            const char* tpl[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                tpl[pl] = tbase + pl * 2 * KP;
+                asm volatile("" : "+s"(tpl[pl]));
+            }
+            auto issue = [&](const i32x4& cv) {
+                static_for<0, 4>([&](auto M_) {
+                    constexpr int m = decltype(M_)::value;
+                    // 24-bit multiply: pre-split tables are host-checked < 2^24 rows and < 4 GiB
+                    const uint32_t vo = __umul24((uint32_t)cv[m], (uint32_t)PRESPLIT_ROW_BYTES) + ld_off;
+                    static_for<0, 3>([&](auto PL_) {
+                        constexpr int pl = decltype(PL_)::value;
+                        __builtin_amdgcn_global_load_lds((const void*)(tpl[pl] + vo),
+                                                         (lds_void*)(img + (pl * 4 + m) * 1024), 16, 0, 0);
+                    });
+                });
+            };
+            auto read = [&](u32x4 (&P)[3][C]) {
+                static_for<0, 3>([&](auto PL_) {
+                    constexpr int pl = decltype(PL_)::value;
+                    static_for<0, C>([&](auto B_) {
+                        constexpr int b = decltype(B_)::value;
+                        static_for<0, 2>([&](auto H_) {
+                            constexpr int h = decltype(H_)::value;
+                            const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                (lds_s16x4*)(img + rd[b] + (pl * 4 + h) * 1024));
+                            const u32x2 w = __builtin_bit_cast(u32x2, v);
+                            P[pl][b][2 * h] = w[0];
+                            P[pl][b][2 * h + 1] = w[1];
+                        });
+                    });
+                });
+            };
+            if (nblk > 0) {
                 const int lastb = nblk - 1;
-                int v0 = load_cr(0), v1 = load_cr(min(1, lastb));
-                expand_cr(v0, I, R0);
-                gather_blk(I, Y0);
-                v0 = load_cr(min(2, lastb));
-                int b = 0;
-                for (; b + 2 < nblk; b += 2) {
-                    expand_cr(v1, I, R1);
-                    gather_blk(I, Y1);
-                    v1 = load_cr(min(b + 3, lastb));
+                const i32x4* cp = (const i32x4*)(a.col_ps + tk.begin) + r8;          // + 8 per block
+                const u32x4* rp = (const u32x4*)(a.rat_pk + (tk.begin >> 1)) + g;    // + 4 per block
+                i32x4 cv = cp[0];
+                u32x4 Rn = rp[0];
+                issue(cv);
+                cv = cp[8 * min(1, lastb)];
+                for (int b = 0; b < nblk; ++b) {
+                    const u32x4 R = Rn;
+                    u32x4 P[3][C];
+                    read(P);   // the compiler waits for the pending LDS-DMA (vmcnt) before these reads
+                    // the operands are in registers before the image is overwritten by the next block's DMA
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (b < lastb) issue(cv);
+                    cv = cp[8 * min(b + 2, lastb)];
+                    Rn = rp[4 * min(b + 1, lastb)];
                     __builtin_amdgcn_sched_barrier(0);
-                    step(Y0, R0);
+                    mfma_block(P, R);
                     __builtin_amdgcn_sched_barrier(0);
-                    expand_cr(v0, I, R0);
-                    gather_blk(I, Y0);
-                    v0 = load_cr(min(b + 4, lastb));
-                    __builtin_amdgcn_sched_barrier(0);
-                    step(Y1, R1);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                if (nblk - b == 2) {
-                    expand_cr(v1, I, R1);
-                    gather_blk(I, Y1);
-                    __builtin_amdgcn_sched_barrier(0);
-                    step(Y0, R0);
-                    step(Y1, R1);
-                } else {
-                    step(Y0, R0);
-                }
-              }
-            } else if (nblk > 0) {
-                Cols I0, I1;
-                Rats R0, R1;
-                Piece Y0[B], Y1[B];
-                const int lastb = nblk - 1;
-                load_cols(0, I0);
-                load_cols(min(1, lastb), I1);
-                gather_blk(I0, Y0);
-                load_rats(0, R0);
-                load_cols(min(2, lastb), I0);
-                int b = 0;
-                for (; b + 2 < nblk; b += 2) {
-                    gather_blk(I1, Y1);
-                    load_rats(b + 1, R1);
-                    load_cols(min(b + 3, lastb), I1);
-                    __builtin_amdgcn_sched_barrier(0);
-                    step(Y0, R0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    gather_blk(I0, Y0);
-                    load_rats(b + 2, R0);
-                    load_cols(min(b + 4, lastb), I0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    step(Y1, R1);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                if (nblk - b == 2) {
-                    gather_blk(I1, Y1);
-                    load_rats(b + 1, R1);
-                    __builtin_amdgcn_sched_barrier(0);
-                    step(Y0, R0);
-                    step(Y1, R1);
-                } else {
-                    step(Y0, R0);
                 }
             }
+#else
+            // register path: lane (g, j) gathers the [h, m | l] pieces of features 4j..4j+3 of its group's 8
+            // entries and transposes bf16 halves into the operands with v_perm_b32 (48 per block); one 4-B load per
+            // lane brings a block's columns (lanes j < 8) and bf16 rating pairs (lanes 8..11), expanded by DPP
+            struct Piece { unsigned w[6]; };
+            typedef int i32x4v __attribute__((ext_vector_type(4)));
+            struct Cols { i32x4v i[2]; };
+            const uint32_t hm_off = 16u * j, l_off = 256u + 8u * j;
+            auto gather_blk = [&](const Cols& x, Piece (&y)[B]) {
+#pragma unroll
+                for (int t = 0; t < B; ++t) {
+                    const uint32_t ro = __umul24((uint32_t)x.i[t >> 2][t & 3], (uint32_t)PRESPLIT_ROW_BYTES);
+                    const u32x4 hm = *(const u32x4*)(tbase + (ro + hm_off));
+                    const u32x2 l = *(const u32x2*)(tbase + (ro + l_off));
+                    y[t].w[0] = hm[0]; y[t].w[1] = hm[1];
+                    y[t].w[2] = hm[2]; y[t].w[3] = hm[3];
+                    y[t].w[4] = l[0]; y[t].w[5] = l[1];
+                }
+            };
+            const int32_t* crb = j < 8 ? a.col + tk.begin + g * B + j
+                                       : (const int32_t*)a.rat_pk + (tk.begin >> 1) + g * 4 + (j & 3);
+            const int cshift = j < 8 ? 5 : 4;   // per-block stride: 32 columns or 16 rating pairs
+            auto load_cr = [&](int blk) { return crb[blk << cshift]; };
+            auto expand_cr = [&](int v, Cols& I, u32x4& R) {
+                static_for<0, 8>([&](auto T) {
+                    constexpr int t = T;
+                    I.i[t >> 2][t & 3] = __builtin_amdgcn_mov_dpp(v, 0x150 + t, 0xf, 0xf, false);
+                });
+                static_for<0, 4>([&](auto Q) {
+                    constexpr int q = Q;
+                    R[q] = (unsigned)__builtin_amdgcn_mov_dpp(v, 0x150 + 8 + q, 0xf, 0xf, false);
+                });
+            };
+            auto transpose = [&](const Piece (&y)[B], u32x4 (&P)[3][C]) {
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                    for (int b = 0; b < C; ++b)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            unsigned v = __builtin_amdgcn_perm(y[2 * q + 1].w[2 * pl + (b >> 1)],
+                                                               y[2 * q].w[2 * pl + (b >> 1)],
+                                                               (b & 1) ? 0x07060302u : 0x05040100u);
+                            pin(v);
+                            P[pl][b][q] = v;
+                        }
+            };
+            if (nblk > 0) {
+                // three waves per SIMD (168 VGPRs): one gather buffer, the other waves hide its latency; the
+                // block's columns/ratings are loaded one block ahead
+                Cols I;
+                u32x4 R;
+                Piece Y[B];
+                const int lastb = nblk - 1;
+                int v = load_cr(0);
+                for (int b = 0; b < nblk; ++b) {
+                    expand_cr(v, I, R);
+                    gather_blk(I, Y);
+                    v = load_cr(min(b + 1, lastb));
+                    __builtin_amdgcn_sched_barrier(0);
+                    u32x4 P[3][C];
+                    transpose(Y, P);
+                    u32x4 Rp;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        unsigned v = R[q];
+                        pin(v);
+                        Rp[q] = v;
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    mfma_block(P, Rp);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+#endif
             // RHS tiles (row i of block b = feature 4i + b, every column equal) -> the per-lane partial layout
             // of the other paths: lane (0, j) holds feature 4j + b, the other rows zero (col_sum restores it)
             wave_sync();
@@ -1947,10 +1968,21 @@ hipError_t launch_pack_ratings(const float* rat, uint32_t* dst, int64_t n_pairs,
     return hipGetLastError();
 }
 hipError_t launch_presplit(const float* src, void* dst, int64_t n_rows, hipStream_t s) {
-    const int64_t pieces = n_rows * 16;
-    if (pieces <= 0) return hipSuccess;
-    als_presplit<<<(unsigned)((pieces + 255) / 256), 256, 0, s>>>(src, (unsigned*)dst, pieces);
+    const int64_t threads = n_rows * (CFK_PRESPLIT_LDS ? 8 : 16);
+    if (threads <= 0) return hipSuccess;
+    als_presplit<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(src, (unsigned*)dst, threads);
     return hipGetLastError();
+}
+hipError_t launch_pack_cols_ps(const int32_t* col, int32_t* dst, int64_t n_entries, hipStream_t s) {
+#if CFK_PRESPLIT_LDS
+    if (n_entries <= 0) return hipSuccess;
+    if (n_entries % BLOCK_ENTRIES) return hipErrorInvalidValue;
+    als_pack_cols_ps<<<(unsigned)((n_entries + 255) / 256), 256, 0, s>>>(col, dst, n_entries);
+    return hipGetLastError();
+#else
+    (void)col; (void)dst; (void)n_entries; (void)s;
+    return hipSuccess;
+#endif
 }
 
 hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s) {
