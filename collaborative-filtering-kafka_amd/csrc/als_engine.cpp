@@ -476,23 +476,27 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     blk.n_tasks = (int32_t)tasks.size();
     blk.n_reduce = (int32_t)reduce.size();
     blk.n_slots = (int32_t)slots;
-    // Pre-split opposite table for the split-bf16 Gram when it stays L2-resident (<= 8 MB as h/m/l pieces,
-    // e.g. the 17,770-row movie table of the user half): 1.5x the gathered bytes from L2, ~3x fewer VALU
-    // instructions per block (measured on the Netflix-shape user half). ALS_PRESPLIT=0/1 forces it.
+    // Pre-split opposite table for the split-bf16 Gram when it stays cache-resident (<= 8 MB as h/m/l planes at
+    // KP = 64: e.g. the 17,770-row movie table of the user half): 1.5x the gathered bytes,
+    // no split VALU (the rows reach LDS by DMA and the MFMA operands come back with transposed reads).
+    // ALS_PRESPLIT=0/1 forces it.
     {
-        const int64_t sb = (n_opp_rows + 1) * (int64_t)cfk::PRESPLIT_ROW_BYTES;
-        bool ps = e->path == Path::MFMA_SPLIT && e->kp == 64 && sb <= (8ll << 20);
-        if (const char* env = getenv("ALS_PRESPLIT")) ps = e->path == Path::MFMA_SPLIT && e->kp == 64 && env[0] == '1';
-        // the pre-split gather forms 32-bit byte offsets row * PRESPLIT_ROW_BYTES with a 24-bit multiply: both the
+        const int64_t sb = (n_opp_rows + 1) * (int64_t)cfk::presplit_row_bytes(e->kp);
+        // KP = 64 only: a KP = 128 variant (24-KB image in the solve-tile area) measured slower at one wave per
+        // SIMD than the interleaved on-the-fly split (profiles/r03g)
+        const bool ps_kp = e->path == Path::MFMA_SPLIT && e->kp == 64;
+        bool ps = ps_kp && sb <= (8ll << 20);
+        if (const char* env = getenv("ALS_PRESPLIT")) ps = ps_kp && env[0] == '1';
+        // the pre-split gather forms 32-bit byte offsets row * presplit_row_bytes with a 24-bit multiply: both the
         // row (< 2^24) and the offset (< 2^32) must fit, also when ALS_PRESPLIT=1 forces the path
         if (n_opp_rows + 1 >= (1 << 24) || sb > (int64_t)UINT32_MAX) ps = false;
         // its RHS multiplies bf16 ratings: integers beyond +-256 are not all bf16 (257 -> 256), so such blocks
         // take the fp32 VALU RHS of the on-the-fly split path instead
         if (max_abs_rating > 256) ps = false;
         blk.presplit = ps;
-        // waves per SIMD of the main launch: the pre-split Gram runs 3 (one gather buffer in 168 VGPRs, the
-        // other waves hide its latency: Netflix-shape user half 4.18 -> 3.84 ms, kbench), the other KP <= 64 MFMA
-        // variants 2 (KP = 128: 1, fixed by the launch)
+        // waves per SIMD of the main launch: the pre-split Gram runs 3 at KP = 64 (168 VGPRs and a 12-KB LDS
+        // image per wave; the other waves hide its latency), the other KP = 32/64 MFMA variants 2 (KP = 128: 1,
+        // fixed by the launch)
         blk.min_waves = ps ? 3 : 2;
         if (ps && (size_t)sb > e->split_bytes) {
             (void)hipFree(e->d_split);
@@ -808,7 +812,7 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
         // the opposite replica is the half's input and does not change between its chunks (als.h): chunk 0
         // converts it, later chunks reuse the conversion
         if (first_chunk)
-            HIP_TRY(cfk::launch_presplit((const float*)opp.ptr, e->d_split, b.n_opp_rows + 1, e->stream));
+            HIP_TRY(cfk::launch_presplit(e->kp, (const float*)opp.ptr, e->d_split, b.n_opp_rows + 1, e->stream));
         a.opp_split = e->d_split;
         a.rat_pk = b.d_rat_pk;
         a.col_ps = b.d_col_ps;

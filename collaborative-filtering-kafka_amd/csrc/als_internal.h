@@ -108,12 +108,13 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
 // Short rows in entry space (als_solve_dual): fp32 split path, kp 64 with cd 2, kp 128 with cd 2 or 4 (rows of
 // 16 * cd padded entries, i.e. cd / 2 blocks); `a.tasks` are FULL tasks of such rows.
 hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s);
-// Pre-split of an fp32 [n_rows][64] factor table (sentinel row included) into the bf16 h/m/l terms the
-// presplit Gram stages in LDS: row r = 384 B at r*384 = three 128-B planes (h, m, l), plane position
-// 16 b + j (b = 0..3, j = 0..15) holding feature 4 j + b, so the 16 values one transposed LDS read hands to a
-// 16-lane group (features 4 j + b, j = 0..15) are 32 contiguous bytes.
-constexpr int PRESPLIT_ROW_BYTES = 384;
-hipError_t launch_presplit(const float* src, void* dst, int64_t n_rows, hipStream_t s);
+// Pre-split of an fp32 [n_rows][kp] factor table (kp = 64 or 128, sentinel row included) into the bf16 h/m/l
+// terms the presplit Gram stages in LDS: row r = presplit_row_bytes(kp) = 6 kp bytes at r * 6 kp = three planes
+// (h, m, l) of 2 kp bytes, plane position 16 b + j (b = 0..kp/16-1, j = 0..15) holding feature (kp/16) j + b, so
+// the 16 values one transposed LDS read hands to a 16-lane group (features (kp/16) j + b, j = 0..15) are 32
+// contiguous bytes.
+__host__ __device__ constexpr int presplit_row_bytes(int kp) { return 6 * kp; }
+hipError_t launch_presplit(int kp, const float* src, void* dst, int64_t n_rows, hipStream_t s);
 // padded column indices -> the per-block order of the presplit gather (n_entries = nnz_padded)
 hipError_t launch_pack_cols_ps(const int32_t* col, int32_t* dst, int64_t n_entries, hipStream_t s);
 // padded fp32 ratings -> bf16 pairs (n_pairs = nnz_padded / 2)

@@ -830,19 +830,12 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 template <int KP>
 constexpr int mfma_waves() { return WAVES; }
 
-// Pre-split Gram with an LDS image (1): the gathered h/m/l rows go straight to LDS by LDS-DMA
-// (global_load_lds_dwordx4) and the MFMA operands come back with transposed reads (ds_read_b64_tr_b16), so no
-// VALU transposes and no gather registers; table layout: b-major planes (als_internal.h). 0: the register path
-// (v_perm_b32 transposes of gathered [h,m | l] pieces), kept as the A/B baseline.
-#ifndef CFK_PRESPLIT_LDS
-#define CFK_PRESPLIT_LDS 1
-#endif
-#if CFK_PRESPLIT_LDS
-// fp32 table -> bf16 h/m/l planes (PRESPLIT_ROW_BYTES per row): thread (row, b, jh) splits features
-// 4 (8 jh + i) + b, i = 0..7, and writes 16 B per plane at position 16 b + 8 jh.
+// fp32 table -> bf16 h/m/l planes (presplit_row_bytes(KP) per row, als_internal.h): thread (row, b, jh) splits
+// features C (8 jh + i) + b, i = 0..7, and writes 16 B per plane at plane position 16 b + 8 jh.
+template <int KP>
 __global__ __launch_bounds__(256) void als_presplit(const float* __restrict__ src, unsigned* __restrict__ dst,
                                                    int64_t n_threads) {
-    constexpr int C = 4, KP = 64;
+    constexpr int C = KP / 16;
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= n_threads) return;
     const int64_t row = t / (2 * C);
@@ -857,7 +850,7 @@ __global__ __launch_bounds__(256) void als_presplit(const float* __restrict__ sr
         m[i] = mm;
         l[i] = ll;
     }
-    unsigned* o = dst + row * (PRESPLIT_ROW_BYTES / 4) + (16 * b + 8 * jh) / 2;
+    unsigned* o = dst + row * (presplit_row_bytes(KP) / 4) + (16 * b + 8 * jh) / 2;
     *(u32x4*)o = h;
     *(u32x4*)(o + 2 * KP / 4) = m;
     *(u32x4*)(o + 4 * KP / 4) = l;
@@ -873,24 +866,6 @@ __global__ __launch_bounds__(256) void als_pack_cols_ps(const int32_t* __restric
     const int k = 16 * (x >> 1) + 8 * (r >> 2) + 4 * (x & 1) + (r & 3);
     dst[i] = col[(i & ~(int64_t)31) + k];
 }
-#else
-// fp32 table -> bf16 h/m/l pieces (PRESPLIT_ROW_BYTES per row), one thread per 16-B row piece.
-__global__ __launch_bounds__(256) void als_presplit(const float* __restrict__ src, unsigned* __restrict__ dst,
-                                                   int64_t n_pieces) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= n_pieces) return;
-    const f32x4 x = *(const f32x4*)(src + t * 4);
-    unsigned h01, m01, l01, h23, m23, l23;
-    split3(x[0], x[1], h01, m01, l01);
-    split3(x[2], x[3], h23, m23, l23);
-    // row = [h, m of 16 pieces: 16 x 16 B][l of 16 pieces: 16 x 8 B], so both gathers of a 16-lane group are
-    // contiguous (16-B and 8-B lane strides)
-    unsigned* o = dst + (t >> 4) * (PRESPLIT_ROW_BYTES / 4);
-    const int j = (int)(t & 15);
-    *(u32x4*)(o + 4 * j) = u32x4{h01, h23, m01, m23};
-    *(u32x2*)(o + 64 + 2 * j) = u32x2{l01, l23};
-}
-#endif
 
 // REDUCE = true: the launch of a half's REDUCE tasks (sum of partial slots + solve), compiled apart from the
 // gather kernel so neither carries the other's code and registers.
@@ -904,7 +879,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
     constexpr int TL = tile_lds_floats<C>();
     __shared__ __attribute__((aligned(16))) float tiles_lds[NW][TL > 0 ? TL : 1];
     // pre-split Gram: one block's LDS image per wave (LDS-DMA target)
-    constexpr int STAGE = (PRESPLIT && !REDUCE && CFK_PRESPLIT_LDS) ? 3 * C * 1024 : 16;
+    constexpr int STAGE = (PRESPLIT && !REDUCE && !tiles_in_lds<C>()) ? 3 * C * 1024 : 16;
     __shared__ __attribute__((aligned(1024))) unsigned char stage_lds[NW][STAGE];
     (void)stage_lds;
 
@@ -999,7 +974,9 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             // every factor row). The RHS Y^T r is 12 more MFMAs (B[k][*] = r_k, so every column of the result holds
             // Y_b^T r; the engine picks this variant only for blocks whose ratings are exact in bf16, |r| <= 256).
             // Chosen for tables that stay L2-resident (the 17,770-row movie table the user half reads).
-            static_assert(C == 4, "pre-split Gram: KP = 64");
+            // written for C = 4 and 8; only KP = 64 is instantiated: at KP = 128 (one wave per SIMD) it measured
+            // slower than the interleaved on-the-fly split (user half 13.5 -> 14.2 ms, profiles/r03g)
+            static_assert(C == 4 || C == 8, "pre-split Gram: KP = 64 or 128");
             typedef int i32x4 __attribute__((ext_vector_type(4)));
             const char* tbase = (const char*)a.opp_split;
             f32x4 racc[C];
@@ -1038,48 +1015,56 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                 }
                 MFMA_DRAIN();
             };
-#if CFK_PRESPLIT_LDS
-            // LDS image of one 32-entry block per wave (12 KB): 12 LDS-DMA instructions (plane pl, entry quarter m)
-            // of 1 KB, instruction (pl, m) = 8 rows x one 128-B plane, lane 8 r + i holding 16-B chunk
-            // i ^ 2 (r >> 1) of the row of entry k = 16 (m >> 1) + 8 (r >> 2) + 4 (m & 1) + (r & 3): whole cache
-            // lines per row for the address unit (8 lines per instruction, as many as the register gathers), and a
-            // chunk swizzle that makes the transposed reads conflict-free. Operand (pl, b) of lane (g, 4 q + p) =
-            // two ds_read_b64_tr_b16 (h = 0, 1: entries 8 g + 4 h + 0..3), lane 4 q + p addressing entry
-            // 8 g + 4 h + q, plane positions 16 b + 4 p .. + 3 (features 4 j + b, j = 4 p .. 4 p + 3); the 16 lanes
-            // of a group receive features j = 0..15 of their 4 entries: exactly the registers the v_perm
-            // transposes built. Same products, same order: bitwise equal to the register path.
+            // LDS image of one 32-entry block per wave (3 C KB: 12 KB at KP = 64, 24 KB at KP = 128): 3 C LDS-DMA
+            // instructions (plane pl, 128-B plane half ph, entry quarter m) of 1 KB, instruction = 8 rows x one
+            // 128-B half plane, lane 8 r + i holding 16-B chunk i ^ 2 (r >> 1) of the row of entry
+            // k = 16 (m >> 1) + 8 (r >> 2) + 4 (m & 1) + (r & 3): whole cache lines per row for the address unit (8
+            // lines per instruction), and a chunk swizzle that makes the transposed reads conflict-free. Operand
+            // (pl, b) of lane (g, 4 q + p) = two ds_read_b64_tr_b16 (h = 0, 1: entries 8 g + 4 h + 0..3), lane
+            // 4 q + p addressing entry 8 g + 4 h + q, plane positions 16 b + 4 p .. + 3 (features C j + b,
+            // j = 4 p .. 4 p + 3); the 16 lanes of a group receive features j = 0..15 of their 4 entries. At KP = 64
+            // these are exactly the registers the former v_perm_b32 transposes of register gathers built (same
+            // products, same order: bitwise equal, profiles/r03c). KP = 128 keeps the image in the wave's solve-tile
+            // area (tiles_lds, 36 KB): the tiles are written only after the last block's reads.
             typedef short s16x4 __attribute__((ext_vector_type(4)));
             typedef __attribute__((address_space(3))) void lds_void;
             typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-            constexpr int IMG = 3 * 4 * 1024;
-            static_assert(sizeof(stage_lds[0]) >= IMG, "stage image");
-            unsigned char* img = stage_lds[uni(wave)];
+            constexpr int NH = C / 4;              // 128-B halves per plane
+            constexpr int IMG = 3 * C * 1024;
+            unsigned char* img;
+            if constexpr (tiles_in_lds<C>()) {
+                static_assert(sizeof(tiles_lds[0]) >= IMG, "stage image in the tile area");
+                img = (unsigned char*)tiles_lds[uni(wave)];
+            } else {
+                static_assert(sizeof(stage_lds[0]) >= IMG, "stage image");
+                img = stage_lds[uni(wave)];
+            }
             const int r8 = lane >> 3;
             const uint32_t ld_off = 16u * (uint32_t)((lane & 7) ^ (2 * (r8 >> 1)));
             const int q = (lane >> 2) & 3, p = lane & 3, rr = 4 * (g & 1) + q;
-            uint32_t rd[C];
+            uint32_t rd[4];   // per feature block b & 3 (the 128-B half b >> 2 is an immediate)
 #pragma unroll
-            for (int b = 0; b < C; ++b)
+            for (int b = 0; b < 4; ++b)
                 rd[b] = 2048u * (uint32_t)(g >> 1) + 16u * (uint32_t)(8 * rr + ((2 * b + (p >> 1)) ^ (2 * (rr >> 1)))) +
                         8u * (uint32_t)(p & 1);
             // per-plane table bases kept in SGPRs (opaque to the optimiser: folded into the per-lane offset they
             // would force 64-bit addresses; an LDS-DMA takes no immediate offset here, it would move the LDS
             // destination too), so every DMA takes the saddr form with one 32-bit lane offset per row
-            const char* tpl[3];
+            const char* tpl[3 * NH];
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) {
-                tpl[pl] = tbase + pl * 2 * KP;
-                asm volatile("" : "+s"(tpl[pl]));
+            for (int x = 0; x < 3 * NH; ++x) {
+                tpl[x] = tbase + (x / NH) * 2 * KP + (x % NH) * 128;
+                asm volatile("" : "+s"(tpl[x]));
             }
             auto issue = [&](const i32x4& cv) {
                 static_for<0, 4>([&](auto M_) {
                     constexpr int m = decltype(M_)::value;
                     // 24-bit multiply: pre-split tables are host-checked < 2^24 rows and < 4 GiB
-                    const uint32_t vo = __umul24((uint32_t)cv[m], (uint32_t)PRESPLIT_ROW_BYTES) + ld_off;
-                    static_for<0, 3>([&](auto PL_) {
-                        constexpr int pl = decltype(PL_)::value;
-                        __builtin_amdgcn_global_load_lds((const void*)(tpl[pl] + vo),
-                                                         (lds_void*)(img + (pl * 4 + m) * 1024), 16, 0, 0);
+                    const uint32_t vo = __umul24((uint32_t)cv[m], (uint32_t)presplit_row_bytes(KP)) + ld_off;
+                    static_for<0, 3 * NH>([&](auto X_) {
+                        constexpr int x = decltype(X_)::value;   // plane x / NH, half x % NH
+                        __builtin_amdgcn_global_load_lds((const void*)(tpl[x] + vo),
+                                                         (lds_void*)(img + (x * 4 + m) * 1024), 16, 0, 0);
                     });
                 });
             };
@@ -1091,7 +1076,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                         static_for<0, 2>([&](auto H_) {
                             constexpr int h = decltype(H_)::value;
                             const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                                (lds_s16x4*)(img + rd[b] + (pl * 4 + h) * 1024));
+                                (lds_s16x4*)(img + rd[b & 3] + ((pl * NH + (b >> 2)) * 4 + h) * 1024));
                             const u32x2 w = __builtin_bit_cast(u32x2, v);
                             P[pl][b][2 * h] = w[0];
                             P[pl][b][2 * h + 1] = w[1];
@@ -1121,81 +1106,6 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
-#else
-            // register path: lane (g, j) gathers the [h, m | l] pieces of features 4j..4j+3 of its group's 8
-            // entries and transposes bf16 halves into the operands with v_perm_b32 (48 per block); one 4-B load per
-            // lane brings a block's columns (lanes j < 8) and bf16 rating pairs (lanes 8..11), expanded by DPP
-            struct Piece { unsigned w[6]; };
-            typedef int i32x4v __attribute__((ext_vector_type(4)));
-            struct Cols { i32x4v i[2]; };
-            const uint32_t hm_off = 16u * j, l_off = 256u + 8u * j;
-            auto gather_blk = [&](const Cols& x, Piece (&y)[B]) {
-#pragma unroll
-                for (int t = 0; t < B; ++t) {
-                    const uint32_t ro = __umul24((uint32_t)x.i[t >> 2][t & 3], (uint32_t)PRESPLIT_ROW_BYTES);
-                    const u32x4 hm = *(const u32x4*)(tbase + (ro + hm_off));
-                    const u32x2 l = *(const u32x2*)(tbase + (ro + l_off));
-                    y[t].w[0] = hm[0]; y[t].w[1] = hm[1];
-                    y[t].w[2] = hm[2]; y[t].w[3] = hm[3];
-                    y[t].w[4] = l[0]; y[t].w[5] = l[1];
-                }
-            };
-            const int32_t* crb = j < 8 ? a.col + tk.begin + g * B + j
-                                       : (const int32_t*)a.rat_pk + (tk.begin >> 1) + g * 4 + (j & 3);
-            const int cshift = j < 8 ? 5 : 4;   // per-block stride: 32 columns or 16 rating pairs
-            auto load_cr = [&](int blk) { return crb[blk << cshift]; };
-            auto expand_cr = [&](int v, Cols& I, u32x4& R) {
-                static_for<0, 8>([&](auto T) {
-                    constexpr int t = T;
-                    I.i[t >> 2][t & 3] = __builtin_amdgcn_mov_dpp(v, 0x150 + t, 0xf, 0xf, false);
-                });
-                static_for<0, 4>([&](auto Q) {
-                    constexpr int q = Q;
-                    R[q] = (unsigned)__builtin_amdgcn_mov_dpp(v, 0x150 + 8 + q, 0xf, 0xf, false);
-                });
-            };
-            auto transpose = [&](const Piece (&y)[B], u32x4 (&P)[3][C]) {
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-                    for (int b = 0; b < C; ++b)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            unsigned v = __builtin_amdgcn_perm(y[2 * q + 1].w[2 * pl + (b >> 1)],
-                                                               y[2 * q].w[2 * pl + (b >> 1)],
-                                                               (b & 1) ? 0x07060302u : 0x05040100u);
-                            pin(v);
-                            P[pl][b][q] = v;
-                        }
-            };
-            if (nblk > 0) {
-                // three waves per SIMD (168 VGPRs): one gather buffer, the other waves hide its latency; the
-                // block's columns/ratings are loaded one block ahead
-                Cols I;
-                u32x4 R;
-                Piece Y[B];
-                const int lastb = nblk - 1;
-                int v = load_cr(0);
-                for (int b = 0; b < nblk; ++b) {
-                    expand_cr(v, I, R);
-                    gather_blk(I, Y);
-                    v = load_cr(min(b + 1, lastb));
-                    __builtin_amdgcn_sched_barrier(0);
-                    u32x4 P[3][C];
-                    transpose(Y, P);
-                    u32x4 Rp;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        unsigned v = R[q];
-                        pin(v);
-                        Rp[q] = v;
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                    mfma_block(P, Rp);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-#endif
             // RHS tiles (row i of block b = feature 4i + b, every column equal) -> the per-lane partial layout
             // of the other paths: lane (0, j) holds feature 4j + b, the other rows zero (col_sum restores it)
             wave_sync();
@@ -1967,22 +1877,19 @@ hipError_t launch_pack_ratings(const float* rat, uint32_t* dst, int64_t n_pairs,
     als_pack_ratings<<<(unsigned)((n_pairs + 255) / 256), 256, 0, s>>>(rat, dst, n_pairs);
     return hipGetLastError();
 }
-hipError_t launch_presplit(const float* src, void* dst, int64_t n_rows, hipStream_t s) {
-    const int64_t threads = n_rows * (CFK_PRESPLIT_LDS ? 8 : 16);
+hipError_t launch_presplit(int kp, const float* src, void* dst, int64_t n_rows, hipStream_t s) {
+    const int64_t threads = n_rows * 2 * (kp / 16);
     if (threads <= 0) return hipSuccess;
-    als_presplit<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(src, (unsigned*)dst, threads);
+    const unsigned grid = (unsigned)((threads + 255) / 256);
+    if (kp != 64) return hipErrorInvalidValue;   // the pre-split Gram is built for KP = 64
+    als_presplit<64><<<grid, 256, 0, s>>>(src, (unsigned*)dst, threads);
     return hipGetLastError();
 }
 hipError_t launch_pack_cols_ps(const int32_t* col, int32_t* dst, int64_t n_entries, hipStream_t s) {
-#if CFK_PRESPLIT_LDS
     if (n_entries <= 0) return hipSuccess;
     if (n_entries % BLOCK_ENTRIES) return hipErrorInvalidValue;
     als_pack_cols_ps<<<(unsigned)((n_entries + 255) / 256), 256, 0, s>>>(col, dst, n_entries);
     return hipGetLastError();
-#else
-    (void)col; (void)dst; (void)n_entries; (void)s;
-    return hipSuccess;
-#endif
 }
 
 hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s) {
