@@ -14,9 +14,10 @@ Prints ONE JSON line (rank 0). `roofline` describes the dominant kernel launch (
 fused gather/Gram/solve launches; both are under roofline.per_launch), timed with HIP events on the stream the
 kernel is launched on. Its `bound` is the launch's real limiter, from the rocprofv3 counters of the same build
 (profiles/counters_k<k>.json, written by tools/prof_summary.py from a profiles/r03*/ pass): the pre-split user
-half and every KP = 128 launch are bound by the MFMA pipe (achieved = the split-bf16 Gram's MFMA flops as issued,
-against the dense bf16 peak), the on-the-fly-split movie half at k = 64 by the fabric gather of the opposite rows
-(counter bytes / time against the Infinity-Cache gather ceiling). The SURVEY.md §8d algorithmic-byte fraction
+half (LDS-DMA rows, transposed-read operands, no split VALU) and every KP = 128 launch are bound by the MFMA pipe
+(achieved = the split-bf16 Gram's MFMA flops as issued, against the dense bf16 peak; gram_phase = the same over the
+Gram's cycle share from the counters), the on-the-fly-split movie half at k = 64 by the fabric gather of the
+opposite rows (counter bytes / time against the Infinity-Cache gather ceiling). The SURVEY.md §8d algorithmic-byte fraction
 stays as a secondary field (cache-served gathers included, so it can exceed 1). `cpu_baseline` times the
 oracle's Java-float restatement of the reference hot path (the "port", one C call per sampled half) on a bounded
 sample of the same workload with the reference's 4 stream threads (BaseKafkaApp.java:51), the box's CPU share
@@ -59,10 +60,10 @@ def half_flops(nnz, n_rows, k):
 def mfma_per_block(kp, presplit):
     """v_mfma_f32_16x16x32_bf16 issued per 32-entry block by the split-bf16 Gram (als_kernels.hip): with C = kp/16
     feature blocks, every off-diagonal tile takes the six partial products hh, hm, mh, hl, lh, mm of the
-    three-term split and every diagonal tile four (mm, hh and the folded hm + hl), plus 3 x C RHS MFMAs when
-    the opposite table is pre-split (the RHS is a VALU FMA otherwise)."""
+    three-term split and every diagonal tile four (mm, hh and the folded hm + hl). The RHS is VALU on both paths
+    (fp32 FMAs on the fly, v_dot2_f32_bf16 on the pre-split operands)."""
     c = kp // 16
-    return 6 * (c * (c - 1) // 2) + 4 * c + (3 * c if presplit else 0)
+    return 6 * (c * (c - 1) // 2) + 4 * c
 
 
 def cpu_model():
@@ -250,7 +251,7 @@ def main():
             # ratings (bf16 pairs on the pre-split path) and the written factor rows
             dual_entries = sum(32 * (c_ + 1) * n for c_, n in enumerate(dual))
             main_entries = main_blocks * 32
-            row_b = 384 if path["presplit"] else 4 * kp
+            row_b = 6 * kp if path["presplit"] else 4 * kp   # pre-split: bf16 h/m/l planes
             gathered = (main_entries * (row_b + 4 + (2 if path["presplit"] else 4)) + dual_entries * (4 * kp + 8)
                         + 4 * kp * i["n_rows"])
             d = {
@@ -279,15 +280,20 @@ def main():
                          limit="fabric gather of the opposite factor rows: PMC FETCH x2 + WRITE bytes / launch time "
                                "against the Infinity-Cache random-row gather ceiling (MI355X_MICROARCH.md)")
             elif path["presplit"]:
-                # gathers served by L2 (the pre-split table is L2-resident): requested bytes against the L2 gather
-                # ceiling; the Gram phase alone (its cycle share from the counters) runs closer to it
-                d.update(bound="gather (L2)", unit="GB/s", peak=L2_GATHER_CEILING_GBS, achieved=gathered / t_s / 1e9,
-                         limit="L2 -> CU gather of the pre-split opposite rows (384 B per entry) in the Gram phase; "
-                               "the solve phase (counters.solve_phase) is latency-bound")
+                # the pre-split Gram issues no split VALU (rows reach LDS by DMA, operands come back by transposed
+                # reads): its limiter is the MFMA pipe; the solve phase after it is latency-bound (counters)
+                d.update(bound="mfma", unit="TFLOP/s", peak=BF16_MFMA_PEAK_TFS, achieved=mf / t_s / 1e12,
+                         limit="MFMA pipe: the split-bf16 Gram's v_mfma_f32_16x16x32_bf16 flops as issued (whole launch, "
+                               "solve phase included) against the dense bf16 peak; gram_phase = the same flops over the "
+                               "Gram's share of the launch cycles (counters.gram_only.cycles_frac); "
+                               "counters.mfma_busy_frac = measured pipe-busy share at the sustained clock")
                 gf = c.get("gram_only", {}).get("cycles_frac")
                 if gf:
-                    d["gram_phase"] = {"achieved_gbs": gathered / (t_s * gf) / 1e9,
-                                       "frac": gathered / (t_s * gf) / 1e9 / L2_GATHER_CEILING_GBS}
+                    d["gram_phase"] = {"achieved_tflops": mf / (t_s * gf) / 1e12,
+                                       "frac": mf / (t_s * gf) / 1e12 / BF16_MFMA_PEAK_TFS,
+                                       "mfma_busy_frac": c.get("gram_only", {}).get("mfma_busy_frac")}
+                d["gather_l2"] = {"achieved_gbs": gathered / t_s / 1e9, "peak": L2_GATHER_CEILING_GBS,
+                                  "frac": gathered / t_s / 1e9 / L2_GATHER_CEILING_GBS}
             else:
                 d.update(bound="mfma", unit="TFLOP/s", peak=BF16_MFMA_PEAK_TFS, achieved=mf / t_s / 1e12,
                          limit="MFMA pipe at one wave per SIMD: the split-bf16 Gram's v_mfma_f32_16x16x32_bf16 flops "

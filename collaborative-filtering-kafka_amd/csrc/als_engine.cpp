@@ -263,7 +263,14 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
 #endif
     if (const char* env = getenv("ALS_DEBUG_REDUCE_GEN_SKEW")) e->debug_gen_skew = (uint32_t)atoi(env);
     if (const char* env = getenv("ALS_DEBUG_FIXED_GEN")) e->debug_fixed_gen = env[0] == '1';
-    if (const char* env = getenv("ALS_REFINE_MIN_PIVOT")) e->refine_min_pivot = (float)atof(env);
+    if (const char* env = getenv("ALS_REFINE_MIN_PIVOT")) {
+        // the product library can only refine MORE often than the validated gate (> 1: every row); thresholds
+        // below 0.45 drop accuracy (tools/refine_accuracy.py) and are accepted by the debug build only
+        e->refine_min_pivot = (float)atof(env);
+#ifndef CFK_DEBUG_KNOBS
+        e->refine_min_pivot = std::max(e->refine_min_pivot, 0.45f);
+#endif
+    }
     if (const char* env = getenv("ALS_DUAL_SIDE")) e->dual_side = env[0] != '0';
     hipError_t st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (st != hipSuccess) {

@@ -577,18 +577,23 @@ def test_comm_init_group_two_gpus(cfk, oracle_mod):
 
 
 def test_gram_variants_vs_oracle(cfk, oracle_mod, monkeypatch):
-    """The two knobs that select other product code paths: ALS_GRAM=f32 (exact v_mfma_f32_16x16x4_f32 Gram
-    instead of the split-bf16 one) at k = 64 and 128 against the fp64 oracle, and ALS_DUAL_SIDE=0 (entry-space
-    launches on the engine stream instead of the side stream) bitwise equal to the default."""
+    """Every knob that selects another product code path, against the fp64 oracle at k = 64 and 128:
+    ALS_GRAM=f32 (exact v_mfma_f32_16x16x4_f32 Gram instead of the split-bf16 one), ALS_PRESPLIT=0 (the k = 64
+    user half on the on-the-fly split instead of the pre-split LDS-DMA Gram; ALS_PRESPLIT=1 is the default there),
+    ALS_REFINE_MIN_PIVOT=2 (the refinement step on every row; the product library clamps lower values to the
+    validated 0.45 gate, so =0 is the default path), and ALS_DUAL_SIDE=0 (entry-space launches on the engine stream
+    instead of the side stream, bitwise equal to the default)."""
     ds, b = _synthetic(cfk, oracle_mod)
     blk = ds.shard_block(1)
+    knobs = ("ALS_GRAM", "ALS_DUAL_SIDE", "ALS_PRESPLIT", "ALS_REFINE_MIN_PIVOT")
     for k in (64, 128):
         F = np.random.default_rng(k).random((len(b.movie.ids), k))
         ref = oracle_mod.update_side(b.user, F, LAM, "f64")
         ref32 = oracle_mod.update_side(b.user, F.astype(np.float32), LAM, "f32")
         outs = {}
-        for env in ({}, {"ALS_GRAM": "f32"}, {"ALS_DUAL_SIDE": "0"}):
-            for name in ("ALS_GRAM", "ALS_DUAL_SIDE"):
+        for env in ({}, {"ALS_GRAM": "f32"}, {"ALS_DUAL_SIDE": "0"}, {"ALS_PRESPLIT": "0"},
+                    {"ALS_REFINE_MIN_PIVOT": "2"}, {"ALS_REFINE_MIN_PIVOT": "0"}):
+            for name in knobs:
                 monkeypatch.delenv(name, raising=False)
             for name, v in env.items():
                 monkeypatch.setenv(name, v)
@@ -600,6 +605,7 @@ def test_gram_variants_vs_oracle(cfk, oracle_mod, monkeypatch):
             assert np.percentile(rel, 99) <= max(2 * np.percentile(rel_ref, 99), 2e-5), k
             assert rel.max() <= max(3 * rel_ref.max(), 1e-4), k
         assert np.array_equal(outs[()], outs[(("ALS_DUAL_SIDE", "0"),)]), k
+        assert np.array_equal(outs[()], outs[(("ALS_REFINE_MIN_PIVOT", "0"),)]), k   # clamped to the gate
 
 
 def test_entry_space_only_for_rows_not_longer_than_k(cfk, oracle_mod):

@@ -99,11 +99,17 @@ def main(tag, name):
                              "write_bytes": write[role]["WRITE_SIZE"] * 1024}
             traffic[role]["hbm_bytes"] = traffic[role]["fetch_bytes_x2"] + traffic[role]["write_bytes"]
     out["traffic"] = traffic
-    for pas in ("sq", "sq_gram"):
+    for pas in ("sq", "sq_gram", "lds"):
         sq = per_role(f"{src}/{pas}/**/*counter_collection.csv")
         res = {}
         for role, c in sq.items():
             d = dict(c)
+            if "SQ_LDS_BANK_CONFLICT" in c and "SQ_LDS_IDX_ACTIVE" in c and c["SQ_LDS_IDX_ACTIVE"] > 0:
+                d["lds_bank_conflict_frac"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
+            if "SQ_LDS_IDX_ACTIVE" in c and "GRBM_GUI_ACTIVE" in c:
+                d["lds_active_frac"] = c["SQ_LDS_IDX_ACTIVE"] / (c["GRBM_GUI_ACTIVE"] / 8 * 256)   # per CU
+            if "SQ_WAIT_INST_LDS" in c and "SQ_WAVE_CYCLES" in c:
+                d["wait_inst_lds_frac"] = c["SQ_WAIT_INST_LDS"] / c["SQ_WAVE_CYCLES"]
             if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "GRBM_GUI_ACTIVE" in c:
                 # MFMA busy cycles are summed over all SIMDs (1024); GRBM_GUI_ACTIVE over the 8 XCDs
                 d["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8 * 1024)
@@ -147,6 +153,9 @@ def main(tag, name):
                         "mfma_busy_frac": (sq["SQ_VALU_MFMA_BUSY_CYCLES"] - gr["SQ_VALU_MFMA_BUSY_CYCLES"]) / (scyc * SIMDS),
                         "valu_issue_frac": (sq["SQ_INSTS_VALU"] - gr["SQ_INSTS_VALU"]) / (scyc * SIMDS),
                         "note": "whole launch minus the Gram-only launch of the same blocks (debug build)"}
+        ld = out.get("lds", {}).get(side)
+        if ld:
+            d["lds"] = {x: ld[x] for x in ("lds_bank_conflict_frac", "lds_active_frac", "wait_inst_lds_frac") if x in ld}
         per_side[side] = d
     json.dump({"k": k, "nnz": cfg.get("nnz", 100_000_000), "per_side": per_side, "source": f"profiles/{name}",
                "note": "per launch; hbm_bytes = FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> B (Infinity-Cache "

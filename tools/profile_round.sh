@@ -3,6 +3,7 @@
 #   bench.json            the default bench.py line (200 timed steps, CPU baseline included)
 #   trace/                rocprofv3 --kernel-trace --stats of a 20-step bench run (kernel_stats.csv)
 #   fetch/, write/        one PMC pass each: FETCH_SIZE, WRITE_SIZE (they cannot share a pass)
+#   lds/                  LDS counters (bank-conflict and LDS-array cycles, LDS issue stalls) of the full launches
 #   sq/, sq_gram/         SQ counters of the full launches, and of the Gram alone (ALS_DEBUG_SKIP_SOLVE=1, which only
 #                         the debug build honours: collaborative-filtering-kafka_amd/build_debug, `make debug`)
 # Every GPU step has its own time limit; a fault, abort or timeout ends the script (no further GPU step).
@@ -30,4 +31,6 @@ SQ="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_AN
 step 300 sq.log rocprofv3 --pmc $SQ -d "$O/sq" -o run --output-format csv -- python3 "$R/bench.py" $P
 CFK_ALS_LIB=$R/collaborative-filtering-kafka_amd/build_debug/libcfk_als.so ALS_DEBUG_SKIP_SOLVE=1 \
     step 300 sq_gram.log rocprofv3 --pmc $SQ -d "$O/sq_gram" -o run --output-format csv -- python3 "$R/bench.py" $P
+LDS="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_VALU_MFMA_COEXEC_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
+step 300 lds.log rocprofv3 --pmc $LDS -d "$O/lds" -o run --output-format csv -- python3 "$R/bench.py" $P
 echo "profile_round $tag done"
