@@ -60,10 +60,10 @@ def half_flops(nnz, n_rows, k):
 def mfma_per_block(kp, presplit):
     """v_mfma_f32_16x16x32_bf16 issued per 32-entry block by the split-bf16 Gram (als_kernels.hip): with C = kp/16
     feature blocks, every off-diagonal tile takes the six partial products hh, hm, mh, hl, lh, mm of the
-    three-term split and every diagonal tile four (mm, hh and the folded hm + hl). The RHS is VALU on both paths
-    (fp32 FMAs on the fly, v_dot2_f32_bf16 on the pre-split operands)."""
+    three-term split and every diagonal tile four (mm, hh and the folded hm + hl), plus 3 x C RHS MFMAs when
+    the opposite table is pre-split (the RHS is a VALU FMA otherwise)."""
     c = kp // 16
-    return 6 * (c * (c - 1) // 2) + 4 * c
+    return 6 * (c * (c - 1) // 2) + 4 * c + (3 * c if presplit else 0)
 
 
 def cpu_model():

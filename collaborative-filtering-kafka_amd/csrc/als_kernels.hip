@@ -971,22 +971,17 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
         };
         if constexpr (PRESPLIT) {
             // Split-bf16 Gram over a PRE-SPLIT opposite table (als_presplit, once per half: the h/m/l bf16 terms of
-            // every factor row). The RHS Y^T r comes from v_dot2_f32_bf16 on the same operand registers: lane (g, j)
-            // accumulates r_e (h + m + l)_e over its group's entries e = 8g..8g+7 for feature C j + b, 4 x 3 x C dot2
-            // per block (every bf16 x bf16 product exact in fp32; the engine picks this variant only for blocks whose
-            // ratings are exact in bf16, |r| <= 256), and the per-lane partials are the RHS layout of the other paths
-            // (the solve's col_sum adds the 4 groups). 3 C RHS MFMAs with 16 identical result columns would do the
-            // same work 16 times over. Chosen for tables that stay L2-resident (the 17,770-row movie table the user
-            // half reads).
+            // every factor row). The RHS Y^T r is 12 more MFMAs (B[k][*] = r_k, so every column of the result holds
+            // Y_b^T r; the engine picks this variant only for blocks whose ratings are exact in bf16, |r| <= 256).
+            // Chosen for tables that stay L2-resident (the 17,770-row movie table the user half reads).
             // written for C = 4 and 8; only KP = 64 is instantiated: at KP = 128 (one wave per SIMD) it measured
             // slower than the interleaved on-the-fly split (user half 13.5 -> 14.2 ms, profiles/r03g)
             static_assert(C == 4 || C == 8, "pre-split Gram: KP = 64 or 128");
             typedef int i32x4 __attribute__((ext_vector_type(4)));
             const char* tbase = (const char*)a.opp_split;
-            typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-            float rsum[C];
+            f32x4 racc[C];
 #pragma unroll
-            for (int b = 0; b < C; ++b) rsum[b] = 0.f;
+            for (int b = 0; b < C; ++b) racc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
             // the block's MFMAs on operands P[plane h/m/l][feature block b] (entries 8g..8g+7 of feature 4j + b as
             // bf16 pairs) and the bf16 rating pairs R of the same entries
             auto mfma_block = [&](const u32x4 (&P)[3][C], const u32x4& R) {
@@ -1010,20 +1005,14 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                         t = mfma_k32(P[0][b1], P[0][b2], t);
                         acc.g[tile_index<C>(b1, b2)] = t;
                     }
-                // RHS: dot2 of the operand registers with the rating pairs (VALU beside the MFMAs; they only read
-                // registers the MFMAs read, so no operand hazard)
 #pragma unroll
-                for (int b = 0; b < C; ++b)
-#pragma unroll
-                    for (int pl = 2; pl >= 0; --pl)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            // element copies first: __builtin_bit_cast of an ext_vector element (x[q]) is
-                            // miscompiled by this hipcc (it reads element 0 for every q)
-                            const unsigned pv = P[pl][b][q], rv = R[q];
-                            rsum[b] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, pv),
-                                                                      __builtin_bit_cast(bf16x2, rv), rsum[b], false);
-                        }
+                for (int b = 0; b < C; ++b) {
+                    f32x4 t = racc[b];
+                    t = mfma_k32(P[2][b], R, t);
+                    t = mfma_k32(P[1][b], R, t);
+                    t = mfma_k32(P[0][b], R, t);
+                    racc[b] = t;
+                }
                 MFMA_DRAIN();
             };
             // LDS image of one 32-entry block per wave (3 C KB: 12 KB at KP = 64, 24 KB at KP = 128): 3 C LDS-DMA
@@ -1117,8 +1106,17 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
+            // RHS tiles (row i of block b = feature 4i + b, every column equal) -> the per-lane partial layout
+            // of the other paths: lane (0, j) holds feature 4j + b, the other rows zero (col_sum restores it)
+            wave_sync();
+            if (j == 0) {
 #pragma unroll
-            for (int b = 0; b < C; ++b) acc.rhs[b] = rsum[b];
+                for (int b = 0; b < C; ++b) *(f32x4*)(buf + 16 * b + 4 * g) = racc[b];
+            }
+            wave_sync();
+#pragma unroll
+            for (int b = 0; b < C; ++b) acc.rhs[b] = (g == 0) ? buf[16 * b + j] : 0.f;
+            wave_sync();
         } else if constexpr (SPLIT) {
             // Split-bf16 Gram: one v_mfma_f32_16x16x32_bf16 consumes a whole 32-entry block. Lane (g, j)
             // holds A[i = j][k = 8g + t] = y_t[C*j + b] (its own gathered piece, component b, entry t of its
