@@ -1,27 +1,29 @@
 #!/usr/bin/env python3
 """bench.py -- ALS ratings/sec per full iteration, Netflix-shape k=64 fp32 on 1..8 MI355X (BASELINE.json).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload netflix|powerlaw] [--k 64|128]
+                  [--exchange torch|native]
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
       bench.py --gpus N --steps K --warmup W
 
-A step = one full ALS iteration (movie half + RCCL all-gather + user half + RCCL all-gather) over the
-synthetic Netflix-shape ratings (480,189 users x 17,770 movies x 1e8 ratings, k = 64, lambda = 0.05; seeded
-generator). Inputs are resident in HBM before the timed region. The dataset is fixed as N grows
-(strong scaling): users and movies are sharded by id % N, one process per GPU.
+A step = one full ALS iteration (movie half + RCCL all-gather + user half + RCCL all-gather) over seeded synthetic
+ratings, inputs resident in HBM before the timed region:
+  --workload netflix   (default, the metric's config) 480,189 users x 17,770 movies x 1e8 ratings, lambda = 0.05,
+                       k = 64 (BASELINE configs[2]); --k 128 is configs[3];
+  --workload powerlaw  10M users x 1M items x 2e9 ratings, k = 64 (BASELINE configs[4], an 8-GPU config).
+The dataset is fixed as N grows (strong scaling): users and movies are sharded by id % N, one process per GPU, and
+with N > 1 each process synthesizes only its shard's ratings (~2/N of them: als_dataset_synthetic_*_shard).
 
-Prints ONE JSON line (rank 0). `roofline` describes the dominant kernel launch (the slower of the two halves'
-fused gather/Gram/solve launches; both are under roofline.per_launch), timed with HIP events on the stream the
-kernel is launched on. Its `bound` is the launch's real limiter, from the rocprofv3 counters of the same build
-(profiles/counters_k<k>.json, written by tools/prof_summary.py from a profiles/r03*/ pass): the pre-split user
-half (LDS-DMA rows, transposed-read operands, no split VALU) and every KP = 128 launch are bound by the MFMA pipe
-(achieved = the split-bf16 Gram's MFMA flops as issued, against the dense bf16 peak; gram_phase = the same over the
-Gram's cycle share from the counters), the on-the-fly-split movie half at k = 64 by the fabric gather of the
-opposite rows (counter bytes / time against the Infinity-Cache gather ceiling). The SURVEY.md §8d algorithmic-byte fraction
-stays as a secondary field (cache-served gathers included, so it can exceed 1). `cpu_baseline` times the
-oracle's Java-float restatement of the reference hot path (the "port", one C call per sampled half) on a bounded
-sample of the same workload with the reference's 4 stream threads (BaseKafkaApp.java:51), the box's CPU share
-and all `nproc` CPUs, rank 0 at N = 1 only.
+Prints ONE JSON line (rank 0). `roofline` describes the dominant kernel launch (the slower of the two halves' fused
+gather/Gram/solve launches; both are under roofline.per_launch), timed with HIP events on the stream the kernel is
+launched on, against the ceiling that binds it: the MFMA pipe (the Gram's MFMAs as issued against the dense
+bf16/f16 peak) or the gather of the opposite factor rows (bytes requested / time against the chip's gather ceiling
+for where those rows are served from), whichever the launch is closer to; the algorithmic fp32 TFLOP/s and the
+SURVEY.md §8d algorithmic-byte rate are reported beside it. `counters` / `traffic` come from the rocprofv3 passes
+of the SAME library build (profiles/counters_k<k>.json, stamped with the library's sha256; dropped when the hashes
+differ). `cpu_baseline` times the oracle's Java-float restatement of the reference hot path (the "port") on a
+bounded sample of the same workload with the reference's 4 stream threads (BaseKafkaApp.java:51) and the box's CPU
+share, rank 0 at N = 1 only. `build` names the library that ran (path, sha256, the source digest it was built from).
 """
 from __future__ import annotations
 
@@ -36,14 +38,15 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFS = 157.3        # f32 vector = f32 MFMA dense peak
-BF16_MFMA_PEAK_TFS = 2500.0  # dense bf16 MFMA peak (no sparsity)
+MFMA16_PEAK_TFS = 2500.0     # dense bf16 / f16 MFMA peak (no sparsity; the f16 forms take the bf16 cycles)
 # MI355X_MICROARCH.md "Indexed rows: gather into LDS": uniformly random rows of a 151 MB table (the 123 MB k = 64
 # user table the movie half gathers sits between its 38 MB and 151 MB rows) are served at 7.4-7.9 TB/s chip-wide;
-# rows every workgroup shares from the XCD's L2 (the 6.8 MB pre-split movie table of the user half: 91% L2 hits)
-# at 16.8-18.8 TB/s
+# rows every workgroup shares from the XCD's L2 (the 4.5 MB pre-split movie table of the user half) at 16.8-18.8 TB/s
 IC_GATHER_CEILING_GBS = 7900.0
 L2_GATHER_CEILING_GBS = 18800.0
-MFMA_BF16_FLOP = 16 * 16 * 32 * 2   # one v_mfma_f32_16x16x32_bf16
+L2_RESIDENT_BYTES = 8 << 20  # a gathered table this small stays in every XCD's 4 MiB L2 to most of its rows
+MFMA_FLOP = 16 * 16 * 32 * 2   # one v_mfma_f32_16x16x32_{bf16,f16}
+WORKLOADS = {"netflix": (480_189, 17_770, 100_000_000), "powerlaw": (10_000_000, 1_000_000, 2_000_000_000)}
 
 
 def half_bytes(nnz, n_rows, k, s=4):
@@ -58,12 +61,14 @@ def half_flops(nnz, n_rows, k):
 
 
 def mfma_per_block(kp, presplit):
-    """v_mfma_f32_16x16x32_bf16 issued per 32-entry block by the split-bf16 Gram (als_kernels.hip): with C = kp/16
-    feature blocks, every off-diagonal tile takes the six partial products hh, hm, mh, hl, lh, mm of the
-    three-term split and every diagonal tile four (mm, hh and the folded hm + hl), plus 3 x C RHS MFMAs when
-    the opposite table is pre-split (the RHS is a VALU FMA otherwise)."""
+    """16x16x32 MFMAs issued per 32-entry block by the Gram (als_kernels.hip), C = kp/16 feature blocks:
+    pre-split (scaled two-term fp16): 3 per off-diagonal tile (hh, hm, mh), 2 per diagonal tile (hh + the folded
+    hm), 2 C for the RHS (h and m against the rh / rm rating columns); on-the-fly three-term bf16 split: 6 per
+    off-diagonal tile, 4 per diagonal tile, RHS on the VALU."""
     c = kp // 16
-    return 6 * (c * (c - 1) // 2) + 4 * c + (3 * c if presplit else 0)
+    if presplit:
+        return 3 * (c * (c - 1) // 2) + 2 * c + 2 * c
+    return 6 * (c * (c - 1) // 2) + 4 * c
 
 
 def cpu_model():
@@ -76,7 +81,27 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(ds, k, lam, seconds, thread_counts):
+def cpu_share():
+    """CPUs this process may use: the affinity mask, capped by the cgroup CPU quota and by OMP_NUM_THREADS (the GPU
+    box sets it to the box's share; nproc there shows the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    src = [f"affinity {n}"]
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            c = max(1, int(int(q) / int(p)))
+            src.append(f"cgroup cpu.max {c}")
+            n = min(n, c)
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp > 0:
+        src.append(f"OMP_NUM_THREADS {omp}")
+        n = min(n, omp)
+    return n, ", ".join(src)
+
+
+def cpu_baseline(ds, k, lam, seconds, thread_counts, share_src):
     """The oracle's f32 (Java-float, EJML-order) restatement of MFeatureCalculator/UFeatureCalculator on a
     bounded random sample of rows of BOTH halves with equal rating counts R: ratings/s per full iteration =
     R / (t_movie_sample + t_user_sample), once per thread count."""
@@ -130,18 +155,36 @@ def cpu_baseline(ds, k, lam, seconds, thread_counts):
                       f"{main['threads']} threads = the reference's NUM_STREAM_THREADS (BaseKafkaApp.java:51). "
                       f"Representative: a row costs deg k^2 + k^3 / 3 flops, and rows drawn uniformly carry the "
                       f"half's own degree mix, so ratings / s over the sample estimates the full half's rate",
-            "runs": runs, "cpu_model": cpu_model(), "nproc": os.cpu_count(),
-            "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
+            "runs": runs, "cpu_model": cpu_model(), "cpu_share": share_src, "nproc": os.cpu_count()}
 
 
-def load_counters(k, nnz):
-    """Per-launch rocprofv3 counters of this build at (k, nnz): profiles/counters_k<k>.json (tools/prof_summary.py)."""
+def build_record():
+    """The library this process loaded: path, sha256, and the build stamp it carries (source digest)."""
+    import __graft_entry__
+    from cfk_amd import _lib
+    path = os.path.realpath(_lib.LIB_PATH)
+    rec = {"lib_path": os.path.relpath(path, ROOT), "lib_sha256": __graft_entry__.sha256_file(path)}
+    info = __graft_entry__.build_info("product")
+    if info and info.get("lib_sha256") == rec["lib_sha256"]:
+        rec["source_sha256"] = info.get("source_sha256")
+        rec["source_matches_tree"] = info.get("source_sha256") == __graft_entry__.source_digest()
+    return rec
+
+
+def load_counters(k, nnz, lib_sha):
+    """Per-launch rocprofv3 counters at (k, nnz) of THIS library build (profiles/counters_k<k>.json, stamped with
+    the profiled library's sha256 by tools/prof_summary.py): (counters, None) or (None, why they were dropped)."""
     path = os.path.join(ROOT, "profiles", f"counters_k{k}.json")
     try:
         c = json.load(open(path))
     except (OSError, ValueError):
-        return None
-    return c if c.get("k") == k and c.get("nnz") == nnz else None
+        return None, f"no {os.path.relpath(path, ROOT)}"
+    if c.get("k") != k or c.get("nnz") != nnz:
+        return None, f"{os.path.relpath(path, ROOT)} was profiled at k={c.get('k')} nnz={c.get('nnz')}"
+    if c.get("lib_sha256") != lib_sha:
+        return None, (f"stale: {c.get('source')} profiled library {str(c.get('lib_sha256'))[:12]} != this build "
+                      f"{lib_sha[:12]}")
+    return c, None
 
 
 def main():
@@ -149,10 +192,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", choices=tuple(WORKLOADS), default="netflix")
     ap.add_argument("--k", type=int, default=64)
-    ap.add_argument("--users", type=int, default=480_189)
-    ap.add_argument("--movies", type=int, default=17_770)
-    ap.add_argument("--nnz", type=int, default=100_000_000)
+    ap.add_argument("--users", type=int, default=None)
+    ap.add_argument("--movies", type=int, default=None)
+    ap.add_argument("--nnz", type=int, default=None)
     ap.add_argument("--seed", type=int, default=0xA15)
     ap.add_argument("--lam", type=float, default=0.05)
     ap.add_argument("--cpu-seconds", type=float, default=7.0, help="CPU baseline seconds per thread count")
@@ -166,6 +210,13 @@ def main():
                     help="N > 1 ranks all on cuda:0 over gloo: rehearses the multi-rank driver on a one-GPU box "
                          "(RCCL needs one GPU per rank); not a performance configuration")
     args = ap.parse_args()
+    users, movies, nnz_total = WORKLOADS[args.workload]
+    users, movies = args.users or users, args.movies or movies
+    nnz_total = args.nnz or nnz_total
+
+    lib_env = os.environ.get("CFK_ALS_LIB", "")
+    if "build_debug" in lib_env:
+        sys.exit(f"bench: CFK_ALS_LIB={lib_env} is the diagnostics build (work-dropping knobs): refused")
 
     import torch
     import torch.distributed as dist
@@ -191,13 +242,23 @@ def main():
             dist.barrier()
 
     t_setup = time.perf_counter()
-    ds = cfk.Dataset.synthetic_netflix(args.users, args.movies, args.nnz, args.seed, nthreads=min(16, os.cpu_count()))
-    nm, nu, nnz = ds.counts()
+    nthreads = min(16, os.cpu_count() or 1)
+    if world > 1:   # this rank's ratings only (both sides' in-blocks of shard `rank`)
+        ds = cfk.Dataset.synthetic_shard(args.workload, users, movies, nnz_total, args.seed, world, rank, nthreads)
+    elif args.workload == "powerlaw":
+        ds = cfk.Dataset.synthetic_powerlaw(users, movies, nnz_total, args.seed, nthreads=nthreads)
+    else:
+        ds = cfk.Dataset.synthetic_netflix(users, movies, nnz_total, args.seed, nthreads=nthreads)
+    nm, nu, nnz_local = ds.counts()
     exchange = args.exchange if world > 1 and not args.rehearse_one_gpu else "torch"
     app = cfk.ALSApp(world, args.k, args.lam, args.steps, precision="f32", seed=42, device=local, rank=rank,
                      world_size=world, overlap_chunks=args.overlap_chunks,
                      exchange=exchange).setup(ds, check_duplicates=False)
     t_setup = time.perf_counter() - t_setup
+    # ranks the exchange spans: the engine's own communicator (native) or the torch process group; RCCL unless the
+    # one-GPU rehearsal runs the group over gloo
+    exchange_world = app.engine.comm_info()[0] if exchange == "native" else (dist.get_world_size() if world > 1 else 1)
+    rccl_world = None if args.rehearse_one_gpu else exchange_world
 
     for _ in range(args.warmup):
         app.iteration()
@@ -229,8 +290,9 @@ def main():
     mse = app.mse()
 
     if rank == 0:
+        build = build_record()
         info = {"movie": app.info[0], "user": app.info[1]}
-        ctr = load_counters(args.k, nnz) if world == 1 else None
+        ctr, ctr_why = load_counters(args.k, nnz_total, build["lib_sha256"]) if world == 1 else (None, "N > 1")
         kp = eng.kp
         per = {}
         for si, side in enumerate(("movie", "user")):
@@ -243,62 +305,53 @@ def main():
             b = half_bytes(i["nnz"], i["n_rows"], args.k)
             gram_f, solve_f = half_flops(i["nnz"], i["n_rows"], args.k)
             t_s = g_ms[side] / 1000.0
-            mf = ((main_blocks * mfma_per_block(kp, path["presplit"]) + dual_mfma) * MFMA_BF16_FLOP
+            mf = ((main_blocks * mfma_per_block(kp, path["presplit"]) + dual_mfma) * MFMA_FLOP
                   if path["gram_path"] == "mfma_split" else 0)
             c = (ctr or {}).get("per_side", {}).get(side, {})
-            # bytes the launch requests from the memory hierarchy: the gathered opposite rows (pre-split: 384 B of
-            # bf16 h/m/l pieces per padded entry; fp32 otherwise, also for the entry-space rows), column indices,
-            # ratings (bf16 pairs on the pre-split path) and the written factor rows
+            # bytes the launch requests from the memory hierarchy: the gathered opposite rows (4 kp B per padded
+            # entry: fp32, or the fp16 h/m planes of the pre-split table -- the same size), column indices,
+            # ratings (fp16 rh / rm pairs on the pre-split path) and the written factor rows
             dual_entries = sum(32 * (c_ + 1) * n for c_, n in enumerate(dual))
             main_entries = main_blocks * 32
-            row_b = 6 * kp if path["presplit"] else 4 * kp   # pre-split: bf16 h/m/l planes
-            gathered = (main_entries * (row_b + 4 + (2 if path["presplit"] else 4)) + dual_entries * (4 * kp + 8)
+            gathered = (main_entries * (4 * kp + 4 + (4 if path["presplit"] else 4)) + dual_entries * (4 * kp + 8)
                         + 4 * kp * i["n_rows"])
+            opp_rows = info["user" if side == "movie" else "movie"]["n_slots"] + 1
+            table_bytes = opp_rows * 4 * kp
+            gceil = L2_GATHER_CEILING_GBS if table_bytes <= L2_RESIDENT_BYTES else IC_GATHER_CEILING_GBS
+            mfma_frac = mf / t_s / 1e12 / MFMA16_PEAK_TFS if mf else 0.0
+            gather_frac = gathered / t_s / 1e9 / gceil
             d = {
                 "kernel": f"als_solve_mfma<{kp},{1 if kp == 128 else (3 if path['presplit'] else 2)},split,"
-                          f"{'presplit' if path['presplit'] else 'on-the-fly split'}> + als_solve_dual (short rows)",
+                          f"{'presplit f16' if path['presplit'] else 'on-the-fly bf16 split'}> + als_solve_dual "
+                          f"(short rows)",
                 "avg_launch_ms": g_ms[side], "reduce_launch_ms": r_ms[side],
-                "gathered_bytes": gathered,
-                "mfma_bf16": {"per_32_entry_block": mfma_per_block(kp, path["presplit"]),
-                              "flop_per_launch": mf, "executed_tflops": mf / t_s / 1e12, "peak": BF16_MFMA_PEAK_TFS,
-                              "frac": mf / t_s / 1e12 / BF16_MFMA_PEAK_TFS},
+                "mfma": {"per_32_entry_block": mfma_per_block(kp, path["presplit"]), "flop_per_launch": mf,
+                         "executed_tflops": mf / t_s / 1e12, "peak": MFMA16_PEAK_TFS, "frac": mfma_frac},
+                "gather": {"bytes": gathered, "opposite_table_bytes": table_bytes, "achieved_gbs": gathered / t_s / 1e9,
+                           "ceiling_gbs": gceil, "frac": gather_frac,
+                           "ceiling": "L2-resident rows" if gceil == L2_GATHER_CEILING_GBS else
+                                      "Infinity-Cache random rows"},
                 "algorithmic_bytes": {"bytes": b, "achieved_gbs": b / t_s / 1e9, "frac_of_hbm": b / t_s / 1e9 / HBM_PEAK_GBS,
                                       "note": "SURVEY.md §8d algorithmic bytes / launch time; cache-served gathers "
                                               "included, so it can exceed 1: not a bound"},
                 "algorithmic_fp32": {"gram_flop": gram_f, "solve_flop": solve_f,
-                                     "tflops": (gram_f + solve_f) / t_s / 1e12, "fp32_peak": FP32_PEAK_TFS},
+                                     "tflops": (gram_f + solve_f) / t_s / 1e12, "fp32_peak": FP32_PEAK_TFS,
+                                     "note": "useful fp32 work; the split Gram issues several MFMA products per fp32 "
+                                             "product, so executed_tflops > this"},
                 "short_rows_entry_space": dual,
+                "presplit": path["presplit"],
             }
             if c:
                 d["counters"] = c
                 d["traffic"] = c.get("hbm_bytes")
-            if kp <= 64 and not path["presplit"]:
-                # the fabric gather of the opposite factor rows: L2 misses served by the Infinity Cache / HBM
-                fab = c.get("hbm_bytes")
-                d.update(bound="gather (Infinity Cache)", unit="GB/s", peak=IC_GATHER_CEILING_GBS,
-                         achieved=(fab / t_s / 1e9) if fab else None,
-                         limit="fabric gather of the opposite factor rows: PMC FETCH x2 + WRITE bytes / launch time "
-                               "against the Infinity-Cache random-row gather ceiling (MI355X_MICROARCH.md)")
-            elif path["presplit"]:
-                # the pre-split Gram issues no split VALU (rows reach LDS by DMA, operands come back by transposed
-                # reads): its limiter is the MFMA pipe; the solve phase after it is latency-bound (counters)
-                d.update(bound="mfma", unit="TFLOP/s", peak=BF16_MFMA_PEAK_TFS, achieved=mf / t_s / 1e12,
-                         limit="MFMA pipe: the split-bf16 Gram's v_mfma_f32_16x16x32_bf16 flops as issued (whole launch, "
-                               "solve phase included) against the dense bf16 peak; gram_phase = the same flops over the "
-                               "Gram's share of the launch cycles (counters.gram_only.cycles_frac); "
-                               "counters.mfma_busy_frac = measured pipe-busy share at the sustained clock")
-                gf = c.get("gram_only", {}).get("cycles_frac")
-                if gf:
-                    d["gram_phase"] = {"achieved_tflops": mf / (t_s * gf) / 1e12,
-                                       "frac": mf / (t_s * gf) / 1e12 / BF16_MFMA_PEAK_TFS,
-                                       "mfma_busy_frac": c.get("gram_only", {}).get("mfma_busy_frac")}
-                d["gather_l2"] = {"achieved_gbs": gathered / t_s / 1e9, "peak": L2_GATHER_CEILING_GBS,
-                                  "frac": gathered / t_s / 1e9 / L2_GATHER_CEILING_GBS}
+            if mfma_frac >= gather_frac:
+                d.update(bound="mfma", unit="TFLOP/s", peak=MFMA16_PEAK_TFS, achieved=mf / t_s / 1e12, frac=mfma_frac,
+                         limit="MFMA pipe: the Gram's 16x16x32 MFMA flops as issued (whole launch, solve phase "
+                               "included) against the dense bf16/f16 peak")
             else:
-                d.update(bound="mfma", unit="TFLOP/s", peak=BF16_MFMA_PEAK_TFS, achieved=mf / t_s / 1e12,
-                         limit="MFMA pipe at one wave per SIMD: the split-bf16 Gram's v_mfma_f32_16x16x32_bf16 flops "
-                               "as issued against the dense bf16 peak; counters.mfma_busy_frac = pipe-busy share")
-            d["frac"] = d["achieved"] / d["peak"] if d.get("achieved") else None
+                d.update(bound="gather", unit="GB/s", peak=gceil, achieved=gathered / t_s / 1e9, frac=gather_frac,
+                         limit="gather of the opposite factor rows: bytes requested per launch / launch time against "
+                               f"the chip's {d['gather']['ceiling']} gather ceiling (MI355X_MICROARCH.md)")
             per[side] = d
         dom = max(per, key=lambda s: per[s]["avg_launch_ms"])
         d = per[dom]
@@ -307,44 +360,46 @@ def main():
             "achieved": d["achieved"], "peak": d["peak"],
             "unit": d["unit"], "frac": d["frac"], "traffic": d.get("traffic"),
             "kernel": d["kernel"] + f" ({dom} half, the dominant launch)", "limit": d["limit"],
-            "avg_launch_ms": d["avg_launch_ms"], "counters": d.get("counters"), "gram_phase": d.get("gram_phase"),
+            "avg_launch_ms": d["avg_launch_ms"], "counters": d.get("counters"),
+            "counters_dropped": ctr_why,
+            "algorithmic_fp32_tflops": d["algorithmic_fp32"]["tflops"],
             "algorithmic_bytes_frac": d["algorithmic_bytes"]["frac_of_hbm"],
             "both_halves_algorithmic_gbs": (per["movie"]["algorithmic_bytes"]["bytes"] +
                                             per["user"]["algorithmic_bytes"]["bytes"])
                                            / ((g_ms["movie"] + g_ms["user"]) / 1000.0) / 1e9,
             "per_launch": per,
             "counters_source": (ctr or {}).get("source"),
-            "note": "achieved/frac: the dominant launch against its binding ceiling (limiter; bound = its memory "
-                    "(hbm) or compute (mfma) side): the gathered bytes it requests / launch time against the chip's "
-                    "gather ceiling for where those rows are served from (MI355X_MICROARCH.md), or executed MFMA "
-                    "flops against the dense bf16 peak; traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per launch (HBM / "
-                    "Infinity Cache side); counters = rocprofv3 SQ passes of this build (whole launch, Gram only, and "
-                    "their difference = the solve phase)",
+            "note": "achieved/frac: the dominant launch against the ceiling it is closest to (limiter; bound = its "
+                    "memory (hbm) or compute (mfma) side): executed 16x16x32 MFMA flops against the dense bf16/f16 "
+                    "peak, or the gathered bytes it requests / launch time against the chip's gather ceiling for "
+                    "where those rows are served from (MI355X_MICROARCH.md); traffic = PMC FETCH_SIZE x2 + WRITE_SIZE "
+                    "per launch; counters = rocprofv3 SQ passes of this build",
         }
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-            share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or ncpu   # the box's CPU share (16 on one GPU)
-            counts = []
-            for t in (4, min(share, ncpu), ncpu):                   # reference's stream threads, share, nproc
-                if t not in counts:
-                    counts.append(t)
-            cpu = cpu_baseline(ds, args.k, args.lam, args.cpu_seconds, counts)
-        value = nnz * K / elapsed
+            share, share_src = cpu_share()
+            counts = [4] + ([share] if share != 4 else [])      # reference's stream threads, the box's share
+            cpu = cpu_baseline(ds, args.k, args.lam, args.cpu_seconds, counts, share_src)
+        value = nnz_total * K / elapsed
+        wl = (f"{args.workload}-shape synthetic {nu} users x {nm} movies x {nnz_total} ratings, k={args.k}, "
+              f"lambda={args.lam}, one step = one full ALS iteration")
         line = {
             "metric": "ALS ratings/sec per full iteration, k=64 Netflix-shape, 1/2/4/8 MI355X",
             "value": value, "unit": "ratings/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
             "ms_per_step": elapsed / K * 1000.0, "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded Netflix-shape generator)",
-            "config": {"workload": f"netflix-shape synthetic {nu} users x {nm} movies x {nnz} ratings, k={args.k}, "
-                                   f"lambda={args.lam}, one step = one full ALS iteration",
-                       "n_users": nu, "n_movies": nm, "nnz": nnz, "k": args.k, "lambda": args.lam,
-                       "seed": args.seed, "partitions": world, "parallelism": f"id%{world} shards + RCCL all-gather",
-                       "exchange": exchange if world > 1 else None,
-                       "overlap_chunks": args.overlap_chunks if world > 1 else None},
+            "vs_baseline": None, "dtype": "f32", "data": f"synthetic (seeded {args.workload}-shape generator)",
+            "config": {"workload": wl, "workload_name": args.workload,
+                       "n_users": nu, "n_movies": nm, "nnz": nnz_total, "nnz_this_rank": nnz_local, "k": args.k,
+                       "lambda": args.lam, "seed": args.seed, "partitions": world,
+                       "parallelism": f"id%{world} shards + RCCL all-gather",
+                       "exchange": exchange if world > 1 else None, "rccl_world": rccl_world,
+                       "exchange_world": exchange_world,
+                       "overlap_chunks": args.overlap_chunks if world > 1 else None,
+                       "rehearsal_gloo_one_gpu": bool(args.rehearse_one_gpu)},
             "solves_per_s": (nm + nu) * K / elapsed,
             "mse_after": mse,
             "setup_s": t_setup,
+            "build": build,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

@@ -95,6 +95,8 @@ SIGNATURES = [
     ("als_dataset_from_ratings", _i, [_i64, _pi32, _pi32, _pi16, _ppv]),
     ("als_dataset_synthetic_netflix", _i, [_i64, _i64, _i64, _u64, _i, _ppv]),
     ("als_dataset_synthetic_powerlaw", _i, [_i64, _i64, _i64, _u64, _i, _ppv]),
+    ("als_dataset_synthetic_powerlaw_shard", _i, [_i64, _i64, _i64, _u64, _i, _i, _i, _ppv]),
+    ("als_dataset_synthetic_netflix_shard", _i, [_i64, _i64, _i64, _u64, _i, _i, _i, _ppv]),
     ("als_dataset_destroy", _i, [_vp]),
     ("als_dataset_counts", _i, [_vp, _pi64, _pi64, _pi64]),
     ("als_dataset_ids", _i, [_vp, _i, _pi64]),

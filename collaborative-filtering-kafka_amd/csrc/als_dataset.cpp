@@ -50,6 +50,9 @@ struct als_dataset {
     std::vector<int64_t> ids[2];      // ascending raw ids per side (0 = movie, 1 = user)
     std::vector<int32_t> dense[2];    // per rating: dense (ascending-id rank) index of its movie / user
     int chunks[2] = {1, 1};           // chunk-major slot layout per side (als_dataset_set_slot_chunks)
+    // a shard-restricted synthetic dataset (als_dataset_synthetic_powerlaw_shard) holds only the ratings of its
+    // shard's in-blocks, so U0's rating means come from every user's full rating sum, kept here (per dense user)
+    std::vector<int64_t> user_sum, user_cnt;
 };
 
 namespace {
@@ -322,10 +325,13 @@ struct SynthSpec {
     uint64_t perm_salt;
 };
 
+// G > 1: keep only the ratings of shard `keep` (movie id % G == keep or user id % G == keep: the in-blocks of both
+// sides of that shard) -- the same ratings, in the same relative arrival order, as the full dataset's (G = 1).
 int synthesize(const SynthSpec& sp, int64_t n_users, int64_t n_movies, int64_t nnz, uint64_t seed, int nthreads,
-               als_dataset** out) {
+               als_dataset** out, int G = 1, int keep = 0) {
     if (!out) return report(fail(ALS_ERR_INVALID_ARGUMENT, "out is NULL"));
     *out = nullptr;
+    if (G < 1 || keep < 0 || keep >= G) return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad shard %d of %d", keep, G));
     if (n_users < 1 || n_movies < 1 || n_users > INT32_MAX - 1 || n_movies > INT32_MAX - 1)
         return report(fail(ALS_ERR_INVALID_ARGUMENT, "bad entity counts"));
     if (nnz < std::max(n_users, n_movies) || nnz > n_users * n_movies / 2)
@@ -397,6 +403,115 @@ int synthesize(const SynthSpec& sp, int64_t n_users, int64_t n_movies, int64_t n
     }
     // rating histogram of data_sample_medium.txt: 1: 4.55%, 2: 9.78%, 3: 28.37%, 4: 33.51%, 5: 23.80%
     const double cdf[5] = {0.0455, 0.0455 + 0.0978, 0.0455 + 0.0978 + 0.2837, 0.0455 + 0.0978 + 0.2837 + 0.3351, 1.0};
+    // one user's distinct movies (sorted) and ratings, deterministic per user
+    auto gen_user = [&](int64_t u, int32_t* dst, int16_t* rat, std::vector<int32_t>& stamp) {
+        Rng rng(mix64(seed * 0x9E3779B97F4A7C15ULL + (uint64_t)u));
+        const int64_t d = deg[u];
+        int64_t got = 0, tries = 0;
+        const int64_t max_tries = 64 * d + 100000;
+        while (got < d && tries < max_tries) {
+            ++tries;
+            const int64_t i = (int64_t)rng.below(n_movies);
+            const int32_t m = rng.uniform() < prob[i] ? (int32_t)i : alias[i];
+            if (stamp[m] == (int32_t)u) continue;
+            stamp[m] = (int32_t)u;
+            dst[got++] = m;
+        }
+        for (int64_t m = (int64_t)rng.below(n_movies); got < d; m = (m + 1) % n_movies)   // fallback
+            if (stamp[m] != (int32_t)u) {
+                stamp[m] = (int32_t)u;
+                dst[got++] = (int32_t)m;
+            }
+        std::sort(dst, dst + d);
+        for (int64_t t = 0; t < d; ++t) {
+            const double x = rng.uniform();
+            int r = 0;
+            while (r < 4 && x >= cdf[r]) ++r;
+            rat[t] = (int16_t)(r + 1);
+        }
+    };
+    if (G > 1) {
+        // Shard-restricted: every user's list is generated (the same draws as below), only shard `keep`'s ratings are
+        // kept (about 2/G of nnz instead of the whole matrix per process), plus every user's rating sum (U0) and the
+        // movie degrees (the every-movie-rated guarantee, which the full path enforces with a global fix-up pass: the
+        // restricted path requires that no movie is unrated, true of every configured shape: the rarest configs[4]
+        // item expects ~140 ratings).
+        struct Kept { int32_t m, u; int16_t r; };
+        const int64_t n_chunks = (n_users + 255) / 256;
+        std::vector<std::vector<Kept>> chunk(n_chunks);
+        std::vector<int64_t> usum(n_users, 0), ucnt(n_users, 0);
+        std::vector<std::vector<int64_t>> mdeg_t(nthreads);
+        std::atomic<int64_t> next{0};
+        auto worker = [&](int w) {
+            std::vector<int32_t> stamp(n_movies, -1), lst;
+            std::vector<int16_t> rat;
+            std::vector<int64_t>& mdeg = mdeg_t[w];
+            mdeg.assign(n_movies, 0);
+            for (;;) {
+                const int64_t c = next.fetch_add(1);
+                if (c >= n_chunks) break;
+                for (int64_t u = c * 256; u < std::min<int64_t>(n_users, c * 256 + 256); ++u) {
+                    lst.resize(deg[u]);
+                    rat.resize(deg[u]);
+                    gen_user(u, lst.data(), rat.data(), stamp);
+                    const bool own_user = (u + 1) % G == keep;
+                    for (int64_t t = 0; t < deg[u]; ++t) {
+                        ++mdeg[lst[t]];
+                        usum[u] += rat[t];
+                        if (own_user || (lst[t] + 1) % G == keep) chunk[c].push_back({lst[t], (int32_t)u, rat[t]});
+                    }
+                    ucnt[u] = deg[u];
+                }
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int i = 0; i < nthreads; ++i) pool.emplace_back(worker, i);
+        for (auto& t : pool) t.join();
+        for (int64_t m = 0; m < n_movies; ++m) {
+            int64_t d = 0;
+            for (auto& v : mdeg_t) d += v[m];
+            if (d == 0)
+                return report(fail(ALS_ERR_UNSUPPORTED, "movie %lld unrated: the shard-restricted generator needs every "
+                                   "movie rated (use the full generator)", (long long)m + 1));
+        }
+        mdeg_t.clear();
+        // movie-major arrival order: stable counting sort by movie of the user-major kept ratings
+        std::unique_ptr<als_dataset> ds(new als_dataset());
+        std::vector<int64_t> moff(n_movies + 1, 0);
+        int64_t kept = 0;
+        for (auto& ch : chunk) {
+            kept += (int64_t)ch.size();
+            for (const Kept& k : ch) ++moff[k.m + 1];
+        }
+        for (int64_t m = 0; m < n_movies; ++m) moff[m + 1] += moff[m];
+        ds->movie.resize(kept);
+        ds->user.resize(kept);
+        ds->rating.resize(kept);
+        std::vector<int64_t> pos(moff.begin(), moff.end() - 1);
+        for (auto& ch : chunk) {
+            for (const Kept& k : ch) {
+                const int64_t p = pos[k.m]++;
+                ds->movie[p] = k.m + 1;
+                ds->user[p] = k.u + 1;
+                ds->rating[p] = k.r;
+            }
+            std::vector<Kept>().swap(ch);
+        }
+        ds->ids[0].resize(n_movies);
+        ds->ids[1].resize(n_users);
+        std::iota(ds->ids[0].begin(), ds->ids[0].end(), 1);
+        std::iota(ds->ids[1].begin(), ds->ids[1].end(), 1);
+        ds->dense[0].resize(kept);
+        ds->dense[1].resize(kept);
+        for (int64_t t = 0; t < kept; ++t) {
+            ds->dense[0][t] = ds->movie[t] - 1;
+            ds->dense[1][t] = ds->user[t] - 1;
+        }
+        ds->user_sum.swap(usum);
+        ds->user_cnt.swap(ucnt);
+        *out = ds.release();
+        return ALS_OK;
+    }
     // --- per-user distinct movie lists (user-major), deterministic per user ---
     std::vector<int64_t> uoff(n_users + 1, 0);
     for (int64_t u = 0; u < n_users; ++u) uoff[u + 1] = uoff[u] + deg[u];
@@ -410,33 +525,7 @@ int synthesize(const SynthSpec& sp, int64_t n_users, int64_t n_movies, int64_t n
                 const int64_t u0 = next_user.fetch_add(256);
                 if (u0 >= n_users) break;
                 const int64_t u1 = std::min<int64_t>(n_users, u0 + 256);
-                for (int64_t u = u0; u < u1; ++u) {
-                    Rng rng(mix64(seed * 0x9E3779B97F4A7C15ULL + (uint64_t)u));
-                    const int64_t d = deg[u];
-                    int32_t* dst = um.data() + uoff[u];
-                    int64_t got = 0, tries = 0;
-                    const int64_t max_tries = 64 * d + 100000;
-                    while (got < d && tries < max_tries) {
-                        ++tries;
-                        const int64_t i = (int64_t)rng.below(n_movies);
-                        const int32_t m = rng.uniform() < prob[i] ? (int32_t)i : alias[i];
-                        if (stamp[m] == (int32_t)u) continue;
-                        stamp[m] = (int32_t)u;
-                        dst[got++] = m;
-                    }
-                    for (int64_t m = (int64_t)rng.below(n_movies); got < d; m = (m + 1) % n_movies)   // fallback
-                        if (stamp[m] != (int32_t)u) {
-                            stamp[m] = (int32_t)u;
-                            dst[got++] = (int32_t)m;
-                        }
-                    std::sort(dst, dst + d);
-                    for (int64_t t = 0; t < d; ++t) {
-                        const double x = rng.uniform();
-                        int r = 0;
-                        while (r < 4 && x >= cdf[r]) ++r;
-                        ur[uoff[u] + t] = (int16_t)(r + 1);
-                    }
-                }
+                for (int64_t u = u0; u < u1; ++u) gen_user(u, um.data() + uoff[u], ur.data() + uoff[u], stamp);
             }
         };
         std::vector<std::thread> pool;
@@ -518,6 +607,20 @@ int als_dataset_synthetic_powerlaw(int64_t n_users, int64_t n_items, int64_t nnz
     const SynthSpec sp{std::log(mean) - 0.5 * sigma * sigma, sigma, std::max<int64_t>(1, n_items / 10), 0.0, 1.0,
                        0x9A11ULL};
     return synthesize(sp, n_users, n_items, nnz, seed, nthreads, out);
+}
+
+int als_dataset_synthetic_powerlaw_shard(int64_t n_users, int64_t n_items, int64_t nnz, uint64_t seed, int nthreads,
+                                         int n_shards, int shard, als_dataset** out) {
+    const double sigma = 1.5, mean = (double)nnz / (double)std::max<int64_t>(1, n_users);
+    const SynthSpec sp{std::log(mean) - 0.5 * sigma * sigma, sigma, std::max<int64_t>(1, n_items / 10), 0.0, 1.0,
+                       0x9A11ULL};
+    return synthesize(sp, n_users, n_items, nnz, seed, nthreads, out, n_shards, shard);
+}
+
+int als_dataset_synthetic_netflix_shard(int64_t n_users, int64_t n_movies, int64_t nnz, uint64_t seed, int nthreads,
+                                        int n_shards, int shard, als_dataset** out) {
+    const SynthSpec sp{std::log(96.0), std::sqrt(2.0 * std::log(208.2 / 96.0)), 17653, 320.0, 1.85, 0x30F1EULL};
+    return synthesize(sp, n_users, n_movies, nnz, seed, nthreads, out, n_shards, shard);
 }
 
 int als_dataset_destroy(als_dataset* ds) {
@@ -660,9 +763,14 @@ int als_dataset_init_user_factors(const als_dataset* ds, int num_features, uint6
     std::fill(out, out + n_out_rows * ld, 0.f);
     const int64_t nu = (int64_t)ds->ids[1].size();
     std::vector<int64_t> sum(nu, 0), cnt(nu, 0);
-    for (size_t t = 0; t < ds->rating.size(); ++t) {
-        sum[ds->dense[1][t]] += ds->rating[t];
-        ++cnt[ds->dense[1][t]];
+    if (!ds->user_cnt.empty()) {   // shard-restricted synthetic data: the full sums were kept at generation
+        sum = ds->user_sum;
+        cnt = ds->user_cnt;
+    } else {
+        for (size_t t = 0; t < ds->rating.size(); ++t) {
+            sum[ds->dense[1][t]] += ds->rating[t];
+            ++cnt[ds->dense[1][t]];
+        }
     }
     for (int64_t u = 0; u < nu; ++u) {
         float* f = out + m.slot[u] * ld;

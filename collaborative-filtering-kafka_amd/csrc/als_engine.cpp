@@ -45,7 +45,7 @@ struct Block {
     int64_t n_rows = 0, row_offset = 0, n_opp_rows = 0, nnz = 0, nnz_padded = 0;
     int32_t* d_col = nullptr;
     float* d_rat = nullptr;
-    uint32_t* d_rat_pk = nullptr;   // pre-split blocks: ratings as bf16 pairs (the Gram's RHS operand)
+    uint32_t* d_rat_pk = nullptr;   // pre-split blocks: ratings as fp16 rh / rm pairs (the Gram's RHS operand)
     int32_t* d_col_ps = nullptr;    // pre-split blocks: column indices in the LDS-DMA gather order
     Task* d_tasks = nullptr;        // FULL + PARTIAL, sorted by work (longest first)
     Task* d_reduce = nullptr;       // REDUCE
@@ -64,7 +64,7 @@ struct Block {
     std::vector<int32_t> cdoff[3];
     Task* d_sq_tasks = nullptr;     // every FULL + PARTIAL task incl. the short rows (als_sq_error)
     int32_t n_sq = 0;
-    bool presplit = false;          // gather a pre-split (bf16 h/m/l) copy of the opposite table
+    bool presplit = false;          // gather a pre-split (scaled fp16 h/m) copy of the opposite table
     // chunk-major slot layout (als_set_row_layout): local row i -> factor row row_offset + (i / rows_per_chunk) *
     // chunk_stride + i % rows_per_chunk; rows_per_chunk = 0: row_offset + i
     int64_t rows_per_chunk = 0, chunk_stride = 0;
@@ -104,19 +104,20 @@ struct als_engine {
     size_t partial_bytes = 0;
     void* d_split = nullptr;        // pre-split opposite table (cfk::launch_presplit), sized for the larger need
     size_t split_bytes = 0;
+    uint32_t* d_amax = nullptr;     // bits of the pre-split table's largest |x| (cfk::launch_absmax): its scale
     void* h_stage = nullptr;        // pinned staging of als_write_factors / als_read_factors (copy kernels)
     size_t stage_bytes = 0;
     uint32_t* d_integrity = nullptr;   // cfk::INTEGRITY_WORDS: partial slots that failed their check
     uint32_t gen = 0;               // launch generation of the next PARTIAL/REDUCE pair
     int32_t debug_flags = 0;        // debug build only (CFK_DEBUG_KNOBS): ALS_DEBUG_SKIP_SOLVE / _REFINE
-    uint32_t debug_gen_skew = 0;    // ALS_DEBUG_REDUCE_GEN_SKEW=n: REDUCE decodes with generation + n (tests the
-                                    // integrity check: every slot then reads as written by another launch)
+    uint32_t debug_gen_skew = 0;    // debug build only: ALS_DEBUG_REDUCE_GEN_SKEW=n, REDUCE decodes with generation
+                                    // + n (tests the integrity check: every slot reads as written by another launch)
     // ALS_REFINE_MIN_PIVOT (cfk::SolveArgs): 0.45 keeps the worst per-row error ratio to the reference's own fp32
     // path where always refining puts it (0.41, tools/refine_accuracy.py; 0.30 lets it reach 1.2), and skips the
     // step for nearly every Netflix-shape row (k = 128 user half 17.7 -> 14.9 ms); > 1 always refines
     float refine_min_pivot = 0.45f;
-    bool debug_fixed_gen = false;   // ALS_DEBUG_FIXED_GEN=1: every launch uses generation 1, so partial slots of
-                                    // repeated launches are bitwise comparable (als_debug_copy_partials)
+    bool debug_fixed_gen = false;   // debug build only: ALS_DEBUG_FIXED_GEN=1, every launch uses generation 1, so
+                                    // partial slots of repeated launches are bitwise comparable (diagnostics)
     ncclComm_t comm = nullptr;      // RCCL communicator over the G engines (one per GPU) of a sharded run
     int world = 1, rank = 0;
     hipStream_t comm_stream = nullptr;   // all-gathers run here, overlapping the next chunk's solve
@@ -260,9 +261,11 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
         if (env[0] == '1') e->debug_flags |= cfk::SOLVE_FLAG_SKIP_SOLVE;
     if (const char* env = getenv("ALS_DEBUG_SKIP_REFINE"))
         if (env[0] == '1') e->debug_flags |= cfk::SOLVE_FLAG_SKIP_REFINE;
-#endif
+    // integrity fault injection / slot-level diagnostics (tests/test_gpu_integrity.py, tools/split_diag.py): they
+    // weaken the partial-slot check, so they exist in the debug build only
     if (const char* env = getenv("ALS_DEBUG_REDUCE_GEN_SKEW")) e->debug_gen_skew = (uint32_t)atoi(env);
     if (const char* env = getenv("ALS_DEBUG_FIXED_GEN")) e->debug_fixed_gen = env[0] == '1';
+#endif
     if (const char* env = getenv("ALS_REFINE_MIN_PIVOT")) {
         // the product library can only refine MORE often than the validated gate (> 1: every row); thresholds
         // below 0.45 drop accuracy (tools/refine_accuracy.py) and are accepted by the debug build only
@@ -280,9 +283,11 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
     e->own_stream = true;
     st = hipMalloc((void**)&e->d_integrity, cfk::INTEGRITY_WORDS * sizeof(uint32_t));
     if (st == hipSuccess) st = hipMemset(e->d_integrity, 0, cfk::INTEGRITY_WORDS * sizeof(uint32_t));
+    if (st == hipSuccess) st = hipMalloc((void**)&e->d_amax, sizeof(uint32_t));
     if (st != hipSuccess) {
         (void)hipStreamDestroy(e->stream);
         (void)hipFree(e->d_integrity);
+        (void)hipFree(e->d_amax);
         delete e;
         return fail(ALS_ERR_DEVICE, "integrity record: %s", hipGetErrorString(st));
     }
@@ -301,6 +306,7 @@ int als_engine_destroy(als_engine* e) {
     (void)hipFree(e->d_split);
     (void)hipHostFree(e->h_stage);
     (void)hipFree(e->d_integrity);
+    (void)hipFree(e->d_amax);
     for (auto& rec : e->pending)
         for (auto ev : rec.ev) (void)hipEventDestroy(ev);
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
@@ -376,23 +382,14 @@ int check_block_shape(als_engine* e, int64_t n_rows, int64_t row_offset, int64_t
     return ALS_OK;
 }
 
-int max_abs_rating(const int16_t* r, int64_t n) {
-    int m = 0;
-    for (int64_t i = 0; i < n; ++i) m = std::max(m, std::abs((int)r[i]));
-    return m;
-}
-
 // Padded entries of a row of degree d (every row starts on a 32-entry block).
 inline int64_t padded(int64_t d) { return (d + cfk::BLOCK_ENTRIES - 1) / cfk::BLOCK_ENTRIES * cfk::BLOCK_ENTRIES; }
 
 // Work plan of a block whose padded in-block (d_col / d_rat, device, already laid out) has row degrees deg[]
 // and row starts begin[]: FULL / PARTIAL / REDUCE tasks, longest first; uploads the plan, takes ownership of
 // d_col / d_rat and sizes the partial and pre-split workspaces.
-// max_abs_rating: largest |rating| of the block (the pre-split Gram feeds ratings to a bf16 MFMA operand, exact
-// only for |r| <= 256; the reference accepts any Java short, NetflixDataFormatProducer.java:50).
 int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows, int64_t nnz,
-                 const std::vector<int64_t>& deg, const std::vector<int64_t>& begin, int32_t* d_col, float* d_rat,
-                 int max_abs_rating) {
+                 const std::vector<int64_t>& deg, const std::vector<int64_t>& begin, int32_t* d_col, float* d_rat) {
     const int64_t nnz_padded = begin[n_rows];
     auto drop = [&]() {
         (void)hipFree(d_col);
@@ -483,27 +480,21 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     blk.n_tasks = (int32_t)tasks.size();
     blk.n_reduce = (int32_t)reduce.size();
     blk.n_slots = (int32_t)slots;
-    // Pre-split opposite table for the split-bf16 Gram when it stays cache-resident (<= 8 MB as h/m/l planes at
-    // KP = 64: e.g. the 17,770-row movie table of the user half): 1.5x the gathered bytes,
+    // Pre-split opposite table (scaled two-term fp16, cfk::launch_presplit, once per half) for the MFMA Gram at KP = 64
+    // and 128: 4 KP bytes per row (the fp32 row's size), 3 MFMAs per tile instead of the on-the-fly bf16 split's 6,
     // no split VALU (the rows reach LDS by DMA and the MFMA operands come back with transposed reads).
-    // ALS_PRESPLIT=0/1 forces it.
+    // ALS_PRESPLIT=0/1 forces it off/on.
     {
         const int64_t sb = (n_opp_rows + 1) * (int64_t)cfk::presplit_row_bytes(e->kp);
-        // KP = 64 only: a KP = 128 variant (24-KB image in the solve-tile area) measured slower at one wave per
-        // SIMD than the interleaved on-the-fly split (profiles/r03g)
-        const bool ps_kp = e->path == Path::MFMA_SPLIT && e->kp == 64;
-        bool ps = ps_kp && sb <= (8ll << 20);
+        const bool ps_kp = e->path == Path::MFMA_SPLIT && (e->kp == 64 || e->kp == 128);
+        bool ps = ps_kp;
         if (const char* env = getenv("ALS_PRESPLIT")) ps = ps_kp && env[0] == '1';
         // the pre-split gather forms 32-bit byte offsets row * presplit_row_bytes with a 24-bit multiply: both the
         // row (< 2^24) and the offset (< 2^32) must fit, also when ALS_PRESPLIT=1 forces the path
         if (n_opp_rows + 1 >= (1 << 24) || sb > (int64_t)UINT32_MAX) ps = false;
-        // its RHS multiplies bf16 ratings: integers beyond +-256 are not all bf16 (257 -> 256), so such blocks
-        // take the fp32 VALU RHS of the on-the-fly split path instead
-        if (max_abs_rating > 256) ps = false;
         blk.presplit = ps;
-        // waves per SIMD of the main launch: the pre-split Gram runs 3 at KP = 64 (168 VGPRs and a 12-KB LDS
-        // image per wave; the other waves hide its latency), the other KP = 32/64 MFMA variants 2 (KP = 128: 1,
-        // fixed by the launch)
+        // waves per SIMD of the main launch: the pre-split Gram runs 3 at KP = 64 (an 8-KB LDS image per wave; the
+        // other waves hide its latency), the other KP = 32/64 MFMA variants 2 (KP = 128: 1, fixed by the launch)
         blk.min_waves = ps ? 3 : 2;
         if (ps && (size_t)sb > e->split_bytes) {
             (void)hipFree(e->d_split);
@@ -515,10 +506,9 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
             e->split_bytes = (size_t)sb;
         }
         if (ps && nnz_padded > 0) {
-            // the RHS operand's ratings, packed once (setup time): one 4-B load per lane then carries a block's
-            // columns and its bf16 rating pairs (als_kernels.hip, CFK_PRESPLIT_CR)
-            hipError_t st = hipMalloc((void**)&blk.d_rat_pk, (size_t)nnz_padded * 2);
-            if (st != hipSuccess) return fail(ALS_ERR_OUT_OF_MEMORY, "hipMalloc(%lld): %s", (long long)nnz_padded * 2,
+            // the RHS operand's ratings, packed once (setup time): fp16 rh pairs, then rm pairs
+            hipError_t st = hipMalloc((void**)&blk.d_rat_pk, (size_t)nnz_padded * 4);
+            if (st != hipSuccess) return fail(ALS_ERR_OUT_OF_MEMORY, "hipMalloc(%lld): %s", (long long)nnz_padded * 4,
                                               hipGetErrorString(st));
             st = cfk::launch_pack_ratings(blk.d_rat, blk.d_rat_pk, nnz_padded / 2, nullptr);
             // and the column indices in the order of the LDS-DMA gather (one 16-B load per loader row)
@@ -616,8 +606,7 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
             return fail(ALS_ERR_OUT_OF_MEMORY, "in-block upload: %s", hipGetErrorString(st));
         }
     }
-    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat,
-                        max_abs_rating(ratings, nnz));
+    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat);
 }
 
 int als_set_block_coo(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows, int64_t nnz,
@@ -636,8 +625,7 @@ int als_set_block_coo(als_engine* e, int side, int64_t n_rows, int64_t row_offse
     const int code = cfk::build_block_device(rows, cols, ratings, nnz, n_rows, n_opp_rows, e->stream, deg, begin,
                                              &d_col, &d_rat, err);
     if (code != ALS_OK) return fail(code, "als_set_block_coo: %s", err.c_str());
-    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat,
-                        max_abs_rating(ratings, nnz));
+    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat);
 }
 
 int als_alloc_factors(als_engine* e, int side, int64_t n_total_rows) {
@@ -818,11 +806,17 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
     if (b.presplit) {
         // the opposite replica is the half's input and does not change between its chunks (als.h): chunk 0
         // converts it, later chunks reuse the conversion
-        if (first_chunk)
-            HIP_TRY(cfk::launch_presplit(e->kp, (const float*)opp.ptr, e->d_split, b.n_opp_rows + 1, e->stream));
+        if (first_chunk) {
+            const int64_t n_floats = (b.n_opp_rows + 1) * (int64_t)e->kp;
+            HIP_TRY(cfk::launch_absmax((const float*)opp.ptr, n_floats, e->d_amax, e->stream));
+            HIP_TRY(cfk::launch_presplit(e->kp, (const float*)opp.ptr, e->d_split, b.n_opp_rows + 1, e->d_amax,
+                                         e->stream));
+        }
         a.opp_split = e->d_split;
         a.rat_pk = b.d_rat_pk;
+        a.rat_lo_off = b.nnz_padded / 2;
         a.col_ps = b.d_col_ps;
+        a.amax = e->d_amax;
     }
     HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves, b.presplit, false));
     if (side_dual) HIP_TRY(hipStreamWaitEvent(e->side_stream, e->fork, 0));

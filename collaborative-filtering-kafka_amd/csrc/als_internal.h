@@ -55,15 +55,18 @@ struct SolveArgs {
     float lambda;
     int32_t sentinel;       // index of the opposite side's all-zero sentinel row (= n_opp_rows)
     int32_t flags;          // SOLVE_FLAG_* (diagnostics only; 0 in production)
-    const void* opp_split;  // MFMA_SPLIT + presplit: the opposite table as bf16 h/m/l pieces (als_presplit)
+    const void* opp_split;  // MFMA_SPLIT + presplit: the opposite table as fp16 h/m planes (als_presplit)
     uint32_t gen;           // launch generation (PARTIAL and its REDUCE share it): keys the partial-slot encoding
     uint32_t* integrity;    // device record of partial slots that failed their check (see als_kernels.hip)
     float refine_min_pivot; // MFMA tile solve: skip the refinement step when every scaled pivot >= this (> 1: never)
-    const uint32_t* rat_pk; // presplit: the padded ratings as bf16 pairs (entries 2i, 2i+1), exact for |r| <= 256
+    const uint32_t* rat_pk; // presplit: the padded ratings r = rh + rm as fp16 pairs (entries 2i, 2i+1): the rh pairs,
+                            //   then (at rat_lo_off words) the rm pairs; both exact for every Java short
     const int32_t* col_ps;  // presplit: the padded column indices permuted per block for the LDS-DMA gather
                             //   (launch_pack_cols_ps: lane group r of a block loads its 4 rows with one 16-B load)
     int32_t rows_per_chunk; // chunk-major slots (als_set_row_layout): 0 = factor row row_offset + row, else
     int64_t chunk_stride;   //   row_offset + (row / rows_per_chunk) * chunk_stride + row % rows_per_chunk
+    int64_t rat_lo_off;     // presplit: words from the rh pairs to the rm pairs (nnz_padded / 2)
+    const uint32_t* amax;   // presplit: bits of the opposite table's largest |x| (als_absmax): the split scale
 };
 // Factor row of local row `row` under the block's slot layout (wave-uniform: scalar arithmetic, once per task).
 __host__ __device__ inline int64_t factor_row(int64_t row_offset, int32_t rows_per_chunk, int64_t chunk_stride,
@@ -96,8 +99,9 @@ struct SqErrArgs {
 };
 
 // Gram paths: VALU (LDS-staged, fp32 k < 32 and all fp64), MFMA (v_mfma_f32_16x16x4_f32, exact f32
-// products), MFMA_SPLIT (fp32 operands split exactly into three bf16 terms, six v_mfma_f32_16x16x32_bf16
-// partial products per tile, fp32 accumulation: fp32-accurate products at 16x the f32 MFMA rate).
+// products), MFMA_SPLIT (fp32 operands split into narrow terms, fp32 accumulation: fp32-accurate products at a
+// multiple of the f32 MFMA rate): on the fly into three bf16 terms (six v_mfma_f32_16x16x32_bf16 partial products
+// per tile), or -- presplit -- once per half into a scaled two-term fp16 table (three v_mfma_f32_16x16x32_f16).
 enum class Path : int { VALU = 0, MFMA = 1, MFMA_SPLIT = 2 };
 
 // Launch helpers (defined in als_kernels.hip). Return hipSuccess or the launch error.
@@ -108,16 +112,19 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
 // Short rows in entry space (als_solve_dual): fp32 split path, kp 64 with cd 2, kp 128 with cd 2 or 4 (rows of
 // 16 * cd padded entries, i.e. cd / 2 blocks); `a.tasks` are FULL tasks of such rows.
 hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s);
-// Pre-split of an fp32 [n_rows][kp] factor table (kp = 64 or 128, sentinel row included) into the bf16 h/m/l
-// terms the presplit Gram stages in LDS: row r = presplit_row_bytes(kp) = 6 kp bytes at r * 6 kp = three planes
-// (h, m, l) of 2 kp bytes, plane position 16 b + j (b = 0..kp/16-1, j = 0..15) holding feature (kp/16) j + b, so
-// the 16 values one transposed LDS read hands to a 16-lane group (features (kp/16) j + b, j = 0..15) are 32
-// contiguous bytes.
-__host__ __device__ constexpr int presplit_row_bytes(int kp) { return 6 * kp; }
-hipError_t launch_presplit(int kp, const float* src, void* dst, int64_t n_rows, hipStream_t s);
+// Pre-split of an fp32 [n_rows][kp] factor table (kp = 64 or 128, sentinel row included) into the two fp16 terms
+// the presplit Gram stages in LDS: row r = presplit_row_bytes(kp) = 4 kp bytes (the fp32 row's size) at r * 4 kp =
+// two planes (h, m) of 2 kp bytes, plane position 16 b + j (b = 0..kp/16-1, j = 0..15) holding feature (kp/16) j + b
+// scaled by 2^s, so the 16 values one transposed LDS read hands to a 16-lane group (features (kp/16) j + b,
+// j = 0..15) are 32 contiguous bytes. launch_absmax writes the table's largest |x| (bits) to *amax first (zeroed
+// here, on the stream); the presplit kernel and the Gram derive s from it (als_kernels.hip, split_exp).
+__host__ __device__ constexpr int presplit_row_bytes(int kp) { return 4 * kp; }
+hipError_t launch_absmax(const float* src, int64_t n_floats, uint32_t* amax, hipStream_t s);
+hipError_t launch_presplit(int kp, const float* src, void* dst, int64_t n_rows, const uint32_t* amax, hipStream_t s);
 // padded column indices -> the per-block order of the presplit gather (n_entries = nnz_padded)
 hipError_t launch_pack_cols_ps(const int32_t* col, int32_t* dst, int64_t n_entries, hipStream_t s);
-// padded fp32 ratings -> bf16 pairs (n_pairs = nnz_padded / 2)
+// padded fp32 ratings r -> fp16 pairs of rh = f16(r) at dst[0, n_pairs) and of rm = r - rh at dst[n_pairs, 2 n_pairs)
+// (n_pairs = nnz_padded / 2; exact for every integer |r| <= 2^22, so for every Java short)
 hipError_t launch_pack_ratings(const float* rat, uint32_t* dst, int64_t n_pairs, hipStream_t s);
 // bytes % 16 == 0; host_pinned must stay valid until the stream has passed the copy
 hipError_t launch_upload(const void* host_pinned, void* dst, size_t bytes, hipStream_t s);

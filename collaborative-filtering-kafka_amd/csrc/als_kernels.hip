@@ -362,6 +362,38 @@ __device__ __forceinline__ bf16x8 as_bf16x8(const u32x4& v) { return __builtin_b
 __device__ __forceinline__ f32x4 mfma_k32(const u32x4& a, const u32x4& b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b), c, 0, 0, 0);
 }
+
+// Two-term fp16 split of the pre-split tables (als_presplit): x' = x 2^s (s = split_exp of the table's largest |x|,
+// so |x'| <= 2^14), h = f16_rn(x'), m = f16_rn(x' - h). x' - h is exact in fp32 and |x' - h - m| <= 2^-22 |x'|, so
+// h + m carries 22 significant bits of every value. A product is taken as hh + hm + mh (the dropped mm and the
+// representation error are <= 3 2^-22 |x'y'|); every fp16 x fp16 partial product is exact in the fp32 MFMA
+// accumulation. Against the three-term bf16 split (six products) this halves the Gram MFMAs. Its accuracy, with the
+// rest of the solve exact: per-row error 0.07-0.08x the reference's own fp32 EJML error on every test block, equal
+// to rounding the inputs to fp32; the fp32 solve, not the Gram, sets the error.
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void split2(float x0, float x1, unsigned& h, unsigned& m) {
+    const f16x2 hv = __builtin_convertvector(f32x2{x0, x1}, f16x2);
+    const f32x2 hf = __builtin_convertvector(hv, f32x2);
+    const f16x2 mv = __builtin_convertvector(f32x2{x0 - hf[0], x1 - hf[1]}, f16x2);
+    h = __builtin_bit_cast(unsigned, hv);
+    m = __builtin_bit_cast(unsigned, mv);
+}
+__device__ __forceinline__ f32x4 mfma_f16(const u32x4& a, const u32x4& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                  0);
+}
+// Scale exponent s of a pre-split table from the bits of its largest |x| (als_absmax): 2^s max|x| <= 2^14 < the fp16
+// maximum 65504 (no overflow at any rounding), and the table's values use the whole fp16 range (m stays normal for
+// |x| >= 2^-17 max|x|). A zero, infinite or NaN maximum keeps s = 0; s is clamped so 2^s and 2^-2s stay usable.
+__device__ __forceinline__ int split_exp(uint32_t maxbits) {
+    if (maxbits == 0 || maxbits >= 0x7f800000u) return 0;
+    int e = (int)(maxbits >> 23) - 127;          // max in [2^e, 2^(e+1)) (normal)
+    if (e == -127) e = -126;                     // subnormal maximum
+    else if (maxbits & 0x7fffffu) e += 1;        // e = ceil(log2(max))
+    const int s = 14 - e;
+    return s < -100 ? -100 : (s > 100 ? 100 : s);
+}
 // Close a group of v_mfma_f32_16x16x32_bf16: the compiler lets VALU instructions overwrite an MFMA's
 // A/B/C registers one instruction after it (it models the operands as read at issue), which on gfx950
 // intermittently corrupted the Gram (found as run-to-run differences in ~0.1% of rows, tools/determinism.py).
@@ -830,30 +862,43 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 template <int KP>
 constexpr int mfma_waves() { return WAVES; }
 
-// fp32 table -> bf16 h/m/l planes (presplit_row_bytes(KP) per row, als_internal.h): thread (row, b, jh) splits
-// features C (8 jh + i) + b, i = 0..7, and writes 16 B per plane at plane position 16 b + 8 jh.
+// Largest |x| of a table (the pre-split scale, split_exp): grid-stride over 16-B vectors, wave max, one vector-memory
+// atomicMax per wave on the bits (non-negative floats order as unsigned integers). *out is zeroed before the launch.
+__global__ __launch_bounds__(256) void als_absmax(const u32x4* __restrict__ src, int64_t n4, uint32_t* __restrict__ out) {
+    uint32_t m = 0;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+        const u32x4 v = src[i] & 0x7fffffffu;
+        m = max(max(m, max(v[0], v[1])), max(v[2], v[3]));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    if ((threadIdx.x & 63) == 0 && m != 0) atomicMax(out, m);
+}
+
+// fp32 table -> fp16 h/m planes (presplit_row_bytes(KP) per row, als_internal.h) at the table's scale 2^s: thread
+// (row, b, jh) splits features C (8 jh + i) + b, i = 0..7, and writes 16 B per plane at plane position 16 b + 8 jh.
 template <int KP>
 __global__ __launch_bounds__(256) void als_presplit(const float* __restrict__ src, unsigned* __restrict__ dst,
-                                                   int64_t n_threads) {
+                                                   int64_t n_threads, const uint32_t* __restrict__ amax) {
     constexpr int C = KP / 16;
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (t >= n_threads) return;
+    const int sc = split_exp(*amax);
     const int64_t row = t / (2 * C);
     const int b = (int)(t % (2 * C)) >> 1, jh = (int)(t & 1);
     const float* s = src + row * KP + C * 8 * jh + b;
-    u32x4 h, m, l;
+    u32x4 h, m;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        unsigned hh, mm, ll;
-        split3(s[C * (2 * i)], s[C * (2 * i + 1)], hh, mm, ll);
+        unsigned hh, mm;
+        split2(ldexpf(s[C * (2 * i)], sc), ldexpf(s[C * (2 * i + 1)], sc), hh, mm);
         h[i] = hh;
         m[i] = mm;
-        l[i] = ll;
     }
     unsigned* o = dst + row * (presplit_row_bytes(KP) / 4) + (16 * b + 8 * jh) / 2;
     *(u32x4*)o = h;
-    *(u32x4*)(o + 2 * KP / 4) = m;
-    *(u32x4*)(o + 4 * KP / 4) = l;
+    *(u32x4*)(o + KP / 2) = m;   // plane stride 2 KP bytes
 }
 // In-block column indices in the order of the LDS-DMA gather: inside a 32-entry block, word 4 r + x (r = 0..7,
 // x = 0..3) holds the column of entry k = 16 (x >> 1) + 8 (r >> 2) + 4 (x & 1) + (r & 3), so the 8 lanes of loader
@@ -879,7 +924,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
     constexpr int TL = tile_lds_floats<C>();
     __shared__ __attribute__((aligned(16))) float tiles_lds[NW][TL > 0 ? TL : 1];
     // pre-split Gram: one block's LDS image per wave (LDS-DMA target)
-    constexpr int STAGE = (PRESPLIT && !REDUCE && !tiles_in_lds<C>()) ? 3 * C * 1024 : 16;
+    constexpr int STAGE = (PRESPLIT && !REDUCE && !tiles_in_lds<C>()) ? 2 * C * 1024 : 16;
     __shared__ __attribute__((aligned(1024))) unsigned char stage_lds[NW][STAGE];
     (void)stage_lds;
 
@@ -970,67 +1015,61 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             for (int c = 0; c < C; ++c) acc.rhs[c] += r * y[c];
         };
         if constexpr (PRESPLIT) {
-            // Split-bf16 Gram over a PRE-SPLIT opposite table (als_presplit, once per half: the h/m/l bf16 terms of
-            // every factor row). The RHS Y^T r is 12 more MFMAs (B[k][*] = r_k, so every column of the result holds
-            // Y_b^T r; the engine picks this variant only for blocks whose ratings are exact in bf16, |r| <= 256).
-            // Chosen for tables that stay L2-resident (the 17,770-row movie table the user half reads).
-            // written for C = 4 and 8; only KP = 64 is instantiated: at KP = 128 (one wave per SIMD) it measured
-            // slower than the interleaved on-the-fly split (user half 13.5 -> 14.2 ms, profiles/r03g)
+            // Two-term fp16 Gram over a PRE-SPLIT opposite table (als_presplit, once per half: the scaled h/m fp16
+            // terms of every factor row, split2). Tile (b1, b2) takes hh + hm + mh (3 MFMAs), a diagonal tile hh + E
+            // with E = h m^T folded as E + E^T once per task (2 MFMAs). The RHS Y^T r is 2 MFMAs per feature block on
+            // B[k][c] = rh_k (columns 0-7) / rm_k (columns 8-15), r = rh + rm exact in fp16 for every Java short:
+            // column 0 + column 8 = Y_b^T r. KP = 64: 34 MFMAs per 32-entry block (the on-the-fly bf16 split: 52
+            // + VALU RHS); KP = 128: 116 (200 + VALU RHS).
             static_assert(C == 4 || C == 8, "pre-split Gram: KP = 64 or 128");
             typedef int i32x4 __attribute__((ext_vector_type(4)));
+            constexpr int NPL = 2;                 // planes h, m
             const char* tbase = (const char*)a.opp_split;
+            const int sc = split_exp(*a.amax);     // the table's scale 2^sc (wave-uniform scalar load)
             f32x4 racc[C];
 #pragma unroll
             for (int b = 0; b < C; ++b) racc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-            // the block's MFMAs on operands P[plane h/m/l][feature block b] (entries 8g..8g+7 of feature 4j + b as
-            // bf16 pairs) and the bf16 rating pairs R of the same entries
-            auto mfma_block = [&](const u32x4 (&P)[3][C], const u32x4& R) {
+            // the block's MFMAs on operands P[plane h/m][feature block b] (entries 8g..8g+7 of feature C j + b as
+            // fp16 pairs) and the fp16 rating pairs R of the same entries (rh or rm by the lane's column)
+            auto mfma_block = [&](const u32x4 (&P)[NPL][C], const u32x4& R) {
 #pragma unroll
                 for (int b1 = 0; b1 < C; ++b1)
 #pragma unroll
                     for (int b2 = b1; b2 < C; ++b2) {
                         f32x4 t = acc.g[tile_index<C>(b1, b2)];
-                        t = mfma_k32(P[1][b1], P[1][b2], t);
                         if (CFK_DIAG_SYM && b1 == b2) {
-                            f32x4 e = E[b1];
-                            e = mfma_k32(P[0][b1], P[2][b1], e);
-                            e = mfma_k32(P[0][b1], P[1][b1], e);
-                            E[b1] = e;
+                            E[b1] = mfma_f16(P[0][b1], P[1][b1], E[b1]);
                         } else {
-                            t = mfma_k32(P[0][b1], P[2][b2], t);
-                            t = mfma_k32(P[2][b1], P[0][b2], t);
-                            t = mfma_k32(P[0][b1], P[1][b2], t);
-                            t = mfma_k32(P[1][b1], P[0][b2], t);
+                            t = mfma_f16(P[0][b1], P[1][b2], t);
+                            t = mfma_f16(P[1][b1], P[0][b2], t);
                         }
-                        t = mfma_k32(P[0][b1], P[0][b2], t);
+                        t = mfma_f16(P[0][b1], P[0][b2], t);
                         acc.g[tile_index<C>(b1, b2)] = t;
                     }
 #pragma unroll
                 for (int b = 0; b < C; ++b) {
                     f32x4 t = racc[b];
-                    t = mfma_k32(P[2][b], R, t);
-                    t = mfma_k32(P[1][b], R, t);
-                    t = mfma_k32(P[0][b], R, t);
+                    t = mfma_f16(P[1][b], R, t);
+                    t = mfma_f16(P[0][b], R, t);
                     racc[b] = t;
                 }
                 MFMA_DRAIN();
             };
-            // LDS image of one 32-entry block per wave (3 C KB: 12 KB at KP = 64, 24 KB at KP = 128): 3 C LDS-DMA
+            // LDS image of one 32-entry block per wave (2 C KB: 8 KB at KP = 64, 16 KB at KP = 128): 2 C LDS-DMA
             // instructions (plane pl, 128-B plane half ph, entry quarter m) of 1 KB, instruction = 8 rows x one
             // 128-B half plane, lane 8 r + i holding 16-B chunk i ^ 2 (r >> 1) of the row of entry
             // k = 16 (m >> 1) + 8 (r >> 2) + 4 (m & 1) + (r & 3): whole cache lines per row for the address unit (8
             // lines per instruction), and a chunk swizzle that makes the transposed reads conflict-free. Operand
             // (pl, b) of lane (g, 4 q + p) = two ds_read_b64_tr_b16 (h = 0, 1: entries 8 g + 4 h + 0..3), lane
             // 4 q + p addressing entry 8 g + 4 h + q, plane positions 16 b + 4 p .. + 3 (features C j + b,
-            // j = 4 p .. 4 p + 3); the 16 lanes of a group receive features j = 0..15 of their 4 entries. At KP = 64
-            // these are exactly the registers the former v_perm_b32 transposes of register gathers built (same
-            // products, same order: bitwise equal, profiles/r03c). KP = 128 keeps the image in the wave's solve-tile
-            // area (tiles_lds, 36 KB): the tiles are written only after the last block's reads.
+            // j = 4 p .. 4 p + 3); the 16 lanes of a group receive features j = 0..15 of their 4 entries: exactly
+            // the MFMA A/B operand, no lane movement. KP = 128 keeps the image in the wave's solve-tile area
+            // (tiles_lds, 36 KB): the tiles are written only after the last block's reads.
             typedef short s16x4 __attribute__((ext_vector_type(4)));
             typedef __attribute__((address_space(3))) void lds_void;
             typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
             constexpr int NH = C / 4;              // 128-B halves per plane
-            constexpr int IMG = 3 * C * 1024;
+            constexpr int IMG = NPL * C * 1024;
             unsigned char* img;
             if constexpr (tiles_in_lds<C>()) {
                 static_assert(sizeof(tiles_lds[0]) >= IMG, "stage image in the tile area");
@@ -1050,9 +1089,9 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             // per-plane table bases kept in SGPRs (opaque to the optimiser: folded into the per-lane offset they
             // would force 64-bit addresses; an LDS-DMA takes no immediate offset here, it would move the LDS
             // destination too), so every DMA takes the saddr form with one 32-bit lane offset per row
-            const char* tpl[3 * NH];
+            const char* tpl[NPL * NH];
 #pragma unroll
-            for (int x = 0; x < 3 * NH; ++x) {
+            for (int x = 0; x < NPL * NH; ++x) {
                 tpl[x] = tbase + (x / NH) * 2 * KP + (x % NH) * 128;
                 asm volatile("" : "+s"(tpl[x]));
             }
@@ -1061,15 +1100,15 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                     constexpr int m = decltype(M_)::value;
                     // 24-bit multiply: pre-split tables are host-checked < 2^24 rows and < 4 GiB
                     const uint32_t vo = __umul24((uint32_t)cv[m], (uint32_t)presplit_row_bytes(KP)) + ld_off;
-                    static_for<0, 3 * NH>([&](auto X_) {
+                    static_for<0, NPL * NH>([&](auto X_) {
                         constexpr int x = decltype(X_)::value;   // plane x / NH, half x % NH
                         __builtin_amdgcn_global_load_lds((const void*)(tpl[x] + vo),
                                                          (lds_void*)(img + (x * 4 + m) * 1024), 16, 0, 0);
                     });
                 });
             };
-            auto read = [&](u32x4 (&P)[3][C]) {
-                static_for<0, 3>([&](auto PL_) {
+            auto read = [&](u32x4 (&P)[NPL][C]) {
+                static_for<0, NPL>([&](auto PL_) {
                     constexpr int pl = decltype(PL_)::value;
                     static_for<0, C>([&](auto B_) {
                         constexpr int b = decltype(B_)::value;
@@ -1087,15 +1126,20 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             if (nblk > 0) {
                 const int lastb = nblk - 1;
                 const i32x4* cp = (const i32x4*)(a.col_ps + tk.begin) + r8;          // + 8 per block
-                const u32x4* rp = (const u32x4*)(a.rat_pk + (tk.begin >> 1)) + g;    // + 4 per block
+                // rating pairs of the lane's column half: rh (columns 0-7) or rm (columns 8-15)
+                const u32x4* rp = (const u32x4*)(a.rat_pk + (j >= 8 ? a.rat_lo_off : 0) + (tk.begin >> 1)) + g;
                 i32x4 cv = cp[0];
                 u32x4 Rn = rp[0];
                 issue(cv);
                 cv = cp[8 * min(1, lastb)];
                 for (int b = 0; b < nblk; ++b) {
                     const u32x4 R = Rn;
-                    u32x4 P[3][C];
-                    read(P);   // the compiler waits for the pending LDS-DMA (vmcnt) before these reads
+                    u32x4 P[NPL][C];
+                    // every vector-memory op of this wave done: this block's LDS-DMA (and the column / rating loads
+                    // the DMA issue and the MFMAs below need anyway) -- explicit, not left to the compiler's tracking
+                    // of LDS-DMA writes (tests/test_isa_guard.py checks it)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    read(P);
                     // the operands are in registers before the image is overwritten by the next block's DMA
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     if (b < lastb) issue(cv);
@@ -1106,12 +1150,27 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
-            // RHS tiles (row i of block b = feature 4i + b, every column equal) -> the per-lane partial layout
-            // of the other paths: lane (0, j) holds feature 4j + b, the other rows zero (col_sum restores it)
-            wave_sync();
-            if (j == 0) {
+            // back to the table's units: the Gram terms by 2^-2sc, the RHS by 2^-sc (powers of two: exact)
 #pragma unroll
-                for (int b = 0; b < C; ++b) *(f32x4*)(buf + 16 * b + 4 * g) = racc[b];
+            for (int t = 0; t < Acc::NT; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc.g[t][r] = ldexpf(ldexpf(acc.g[t][r], -sc), -sc);
+#pragma unroll
+            for (int b = 0; b < C; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) E[b][r] = ldexpf(ldexpf(E[b][r], -sc), -sc);
+            // RHS tiles (row i of block b = feature C i + b; column 0 = Y^T rh, column 8 = Y^T rm) -> the per-lane
+            // partial layout of the other paths: lane (0, j) holds feature C j + b, the other rows zero (col_sum
+            // restores it)
+            wave_sync();
+#pragma unroll
+            for (int b = 0; b < C; ++b) {
+                f32x4 v = racc[b];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)   // lane (g, 8) += lane (g, 0): DPP row_shr:8
+                    v[r] = ldexpf(v[r] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[r]), 0x118,
+                                                                                    0xf, 0xf, false)), -sc);
+                if (j == 8) *(f32x4*)(buf + 16 * b + 4 * g) = v;
             }
             wave_sync();
 #pragma unroll
@@ -1867,22 +1926,37 @@ hipError_t launch_download(const void* src, void* host_pinned, size_t bytes, hip
     return launch_copy(src, host_pinned, bytes, 1, s);
 }
 
+// r = rh + rm with rh = f16_rn(r), rm = r - rh: both exact fp16 for integers |r| <= 2^22 (every Java short)
 __global__ __launch_bounds__(256) void als_pack_ratings(const float* __restrict__ rat, uint32_t* __restrict__ dst,
                                                         int64_t n_pairs) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < n_pairs) dst[i] = pk_bf16(rat[2 * i], rat[2 * i + 1]);
+    if (i >= n_pairs) return;
+    unsigned h, m;
+    split2(rat[2 * i], rat[2 * i + 1], h, m);
+    dst[i] = h;
+    dst[n_pairs + i] = m;
 }
 hipError_t launch_pack_ratings(const float* rat, uint32_t* dst, int64_t n_pairs, hipStream_t s) {
     if (n_pairs <= 0) return hipSuccess;
     als_pack_ratings<<<(unsigned)((n_pairs + 255) / 256), 256, 0, s>>>(rat, dst, n_pairs);
     return hipGetLastError();
 }
-hipError_t launch_presplit(int kp, const float* src, void* dst, int64_t n_rows, hipStream_t s) {
+hipError_t launch_absmax(const float* src, int64_t n_floats, uint32_t* amax, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(amax, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess || n_floats <= 0) return e;
+    if (n_floats % 4) return hipErrorInvalidValue;   // whole KP-wide rows
+    const int64_t n4 = n_floats / 4;
+    const int64_t blocks = std::min<int64_t>((n4 + 255) / 256, 2048);
+    als_absmax<<<(unsigned)blocks, 256, 0, s>>>((const u32x4*)src, n4, amax);
+    return hipGetLastError();
+}
+hipError_t launch_presplit(int kp, const float* src, void* dst, int64_t n_rows, const uint32_t* amax, hipStream_t s) {
     const int64_t threads = n_rows * 2 * (kp / 16);
     if (threads <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((threads + 255) / 256);
-    if (kp != 64) return hipErrorInvalidValue;   // the pre-split Gram is built for KP = 64
-    als_presplit<64><<<grid, 256, 0, s>>>(src, (unsigned*)dst, threads);
+    if (kp == 64) als_presplit<64><<<grid, 256, 0, s>>>(src, (unsigned*)dst, threads, amax);
+    else if (kp == 128) als_presplit<128><<<grid, 256, 0, s>>>(src, (unsigned*)dst, threads, amax);
+    else return hipErrorInvalidValue;   // the pre-split Gram is built for KP = 64 and 128
     return hipGetLastError();
 }
 hipError_t launch_pack_cols_ps(const int32_t* col, int32_t* dst, int64_t n_entries, hipStream_t s) {
@@ -1916,6 +1990,7 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
             if (kp == 32) return launch_solve_t<float, 32, Path::MFMA_SPLIT, 2>(a, s, reduce);
             if (kp == 64 && presplit) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 3, true>(a, s, reduce);
             if (kp == 64) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2>(a, s, reduce);
+            if (kp == 128 && presplit) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1, true>(a, s, reduce);
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1>(a, s, reduce);
         } else {
             if (kp == 16) return launch_solve_t<float, 16, Path::VALU>(a, s, reduce);

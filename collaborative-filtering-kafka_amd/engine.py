@@ -68,6 +68,16 @@ class Dataset:
         call("als_dataset_synthetic_powerlaw", n_users, n_items, nnz, seed, nthreads, ctypes.byref(h))
         return cls(h.value)
 
+    @classmethod
+    def synthetic_shard(cls, workload: str, n_users: int, n_movies: int, nnz: int, seed: int, n_shards: int,
+                        shard: int, nthreads: int = 0) -> "Dataset":
+        """The same synthetic dataset restricted to the ratings of shard `shard` of n_shards (both sides' in-blocks of
+        that rank): what one process of the G-GPU job needs, ~2/G of the ratings (include/als_host.h)."""
+        h = ctypes.c_void_p()
+        fn = {"netflix": "als_dataset_synthetic_netflix_shard", "powerlaw": "als_dataset_synthetic_powerlaw_shard"}
+        call(fn[workload], n_users, n_movies, nnz, seed, nthreads, n_shards, shard, ctypes.byref(h))
+        return cls(h.value)
+
     def close(self):
         if self._h and self._h.value:
             _lib.lib().als_dataset_destroy(self._h)

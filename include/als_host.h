@@ -51,6 +51,16 @@ int als_dataset_synthetic_netflix(int64_t n_users, int64_t n_movies, int64_t nnz
  * above (exact nnz, no duplicate pairs, every entity rated, ids 1..n, movie-major arrival order). */
 int als_dataset_synthetic_powerlaw(int64_t n_users, int64_t n_items, int64_t nnz, uint64_t seed, int nthreads,
                                    als_dataset** out);
+/* Shard-restricted forms for the one-process-per-GPU driver: the same dataset, but holding only the ratings of
+ * shard `shard` of G = n_shards (movie id % G == shard or user id % G == shard: that rank's in-blocks of both
+ * sides, ~2/G of nnz) in the same relative arrival order, plus every user's rating mean for U0. Every shard query
+ * for `shard` under G, and als_dataset_init_user_factors, return what the full dataset returns; als_dataset_counts
+ * reports all entities but only the kept ratings. Requires every entity rated without the full generator's fix-up
+ * pass (true of the configured shapes; ALS_ERR_UNSUPPORTED otherwise). */
+int als_dataset_synthetic_powerlaw_shard(int64_t n_users, int64_t n_items, int64_t nnz, uint64_t seed, int nthreads,
+                                         int n_shards, int shard, als_dataset** out);
+int als_dataset_synthetic_netflix_shard(int64_t n_users, int64_t n_movies, int64_t nnz, uint64_t seed, int nthreads,
+                                        int n_shards, int shard, als_dataset** out);
 int als_dataset_destroy(als_dataset* ds);
 
 int als_dataset_counts(const als_dataset* ds, int64_t* n_movies, int64_t* n_users, int64_t* nnz);

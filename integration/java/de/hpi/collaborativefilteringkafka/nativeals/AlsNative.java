@@ -7,8 +7,9 @@ package de.hpi.collaborativefilteringkafka.nativeals;
  * org.apache.kafka.streams.errors.StreamsException carrying als_last_error(), which is what the Kafka Streams
  * runtime expects of a failing processor (the reference ignores EJML invert's boolean, MFeatureCalculator.java:98).
  *
- * Arrays are caller-owned and contiguous (GetPrimitiveArrayCritical on the native side); factor matrices are
- * row-major float[] with a row stride of ld floats. Engine handles are als_engine* carried as long.
+ * Arrays are caller-owned; the shim copies them with Get/Set<Type>ArrayRegion (no JNI critical region is held while
+ * a call waits on the GPU). Factor matrices are row-major float[] (double[] for ALS_F64 engines, the fp64 parity
+ * mode) with a row stride of ld elements. Engine handles are als_engine* carried as long.
  * The Java 22+ alternative without a native shim is AlsFfm (Panama FFM).
  */
 public final class AlsNative {
@@ -39,6 +40,10 @@ public final class AlsNative {
     public static native void writeFactors(long engine, int side, long row0, float[] rows, int ld);
     /** als_read_factors (synchronising: device errors surface here) */
     public static native void readFactors(long engine, int side, long row0, float[] out, int ld);
+    /** als_write_factors of an F64 engine (fp64 parity mode) */
+    public static native void writeFactorsF64(long engine, int side, long row0, double[] rows, int ld);
+    /** als_read_factors of an F64 engine */
+    public static native void readFactorsF64(long engine, int side, long row0, double[] out, int ld);
     /** als_solve_half: THE HOT PATH, every row of the side's block (MFeatureCalculator.java:66-104), asynchronous. */
     public static native void solveHalf(long engine, int side, float lambda);
     /** als_synchronize */

@@ -238,3 +238,89 @@ def test_sharded_two_ranks_chunked(tmp_path, oracle_mod, cfk, k):
         assert abs(float(res["mse"]) - mse_o) <= 1e-3
         assert np.linalg.norm(res["U"] - Uo) / np.linalg.norm(Uo) < 1e-3
         assert np.linalg.norm(res["M"] - Mo) / np.linalg.norm(Mo) < 1e-3
+
+
+def _shard_data_worker(rank, world, port, out_dir, workload, restricted):
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    import __graft_entry__
+    cfk = __graft_entry__.load_package()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    shape = (20_000, 1_500, 600_000)
+    if restricted:
+        ds = cfk.Dataset.synthetic_shard(workload, *shape, 5, world, rank, nthreads=8)
+    elif workload == "powerlaw":
+        ds = cfk.Dataset.synthetic_powerlaw(*shape, 5, nthreads=8)
+    else:
+        ds = cfk.Dataset.synthetic_netflix(*shape, 5, nthreads=8)
+    app = cfk.ALSApp(world, 64, LAM, 3, precision="f32", seed=9, device=0, rank=rank, world_size=world,
+                     overlap_chunks=2)
+    app.setup(ds, check_duplicates=False)
+    app.run()
+    U, M = app.factors()
+    np.savez(os.path.join(out_dir, f"{workload}_{int(restricted)}_rank{rank}.npz"), U=U, M=M, mse=app.mse())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("workload", ["netflix", "powerlaw"])
+def test_two_ranks_on_shard_restricted_data(tmp_path, cfk, workload):
+    """bench.py's multi-GPU data path at reduced size: each of 2 ranks (both on cuda:0, gloo carrying the
+    all-gathers, user half in 2 chunks) synthesizes ONLY its shard's ratings (als_dataset_synthetic_*_shard) and
+    the factors and MSE are bitwise those of the same 2-rank run on the full dataset, and equal the 1-rank run's
+    (same per-entity arithmetic; at this size every split row has the same chunking). Multi-GPU RCCL itself is
+    measured only by the driver's 8-GPU run."""
+    import socket
+    import torch.multiprocessing as mp
+    res = {}
+    for restricted in (True, False):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        mp.spawn(_shard_data_worker, args=(2, port, str(tmp_path), workload, restricted), nprocs=2, join=True)
+        res[restricted] = [np.load(os.path.join(tmp_path, f"{workload}_{int(restricted)}_rank{r}.npz")) for r in (0, 1)]
+    shape = (20_000, 1_500, 600_000)
+    ds = (cfk.Dataset.synthetic_powerlaw if workload == "powerlaw" else cfk.Dataset.synthetic_netflix)(*shape, 5, 8)
+    app = cfk.ALSApp(1, 64, LAM, 3, precision="f32", seed=9).setup(ds, check_duplicates=False)
+    app.run()
+    U1, M1 = app.factors()
+    for r in (0, 1):
+        a, b = res[True][r], res[False][r]
+        assert np.array_equal(a["U"], b["U"]) and np.array_equal(a["M"], b["M"]) and float(a["mse"]) == float(b["mse"])
+        assert np.array_equal(a["U"], U1) and np.array_equal(a["M"], M1)
+        assert abs(float(a["mse"]) - app.mse()) <= 1e-12 * app.mse()
+
+
+def test_bench_rehearsal_two_ranks_shard_restricted(tmp_path):
+    """bench.py itself as the driver's N = 2 run launches it (torch.distributed.run, one process per rank), both
+    ranks on cuda:0 over gloo (--rehearse-one-gpu), on the power-law workload at reduced size: one JSON line whose
+    MSE equals the 1-rank bench line's, each rank holding ~2/N of the ratings."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    from conftest import ROOT
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    common = ["--workload", "powerlaw", "--users", "20000", "--movies", "1500", "--nnz", "600000", "--steps", "3",
+              "--warmup", "1", "--no-cpu-baseline"]
+    env = dict(os.environ, OMP_NUM_THREADS="8")
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                          "--gpus", "2", "--rehearse-one-gpu"] + common, capture_output=True, text=True, timeout=300,
+                         env=env, cwd=ROOT)
+    assert two.returncode == 0, two.stderr[-3000:]
+    one = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + common, capture_output=True, text=True,
+                         timeout=300, env=env, cwd=ROOT)
+    assert one.returncode == 0, one.stderr[-3000:]
+    l2 = json.loads([x for x in two.stdout.splitlines() if x.startswith("{")][-1])
+    l1 = json.loads([x for x in one.stdout.splitlines() if x.startswith("{")][-1])
+    assert l2["n_gpus"] == 2 and l2["config"]["exchange_world"] == 2 and l2["config"]["nnz"] == 600_000
+    assert l2["config"]["nnz_this_rank"] < 0.75 * 600_000
+    assert abs(l2["mse_after"] - l1["mse_after"]) <= 1e-9 * l1["mse_after"]
+    assert l1["build"]["lib_sha256"] == l2["build"]["lib_sha256"] and l1["build"]["source_matches_tree"]

@@ -57,29 +57,42 @@ def test_integrity_clean_on_split_rows(cfk, oracle_mod, monkeypatch):
         eng.close()
 
 
-@pytest.mark.parametrize("k,prec", [(64, "f32"), (128, "f32"), (32, "f32"), (10, "f64")])
-def test_integrity_check_catches_foreign_slots(cfk, oracle_mod, monkeypatch, k, prec):
+def test_integrity_check_catches_foreign_slots():
     """Fault injection: the REDUCE launch decodes with another launch's generation (ALS_DEBUG_REDUCE_GEN_SKEW),
     which is exactly what a slot still holding an earlier launch's sums looks like. Every such read must be
-    caught, reported with its slot and row, and cleared by a reset."""
-    monkeypatch.setenv("ALS_CHUNK", "64")
-    monkeypatch.setenv("ALS_DEBUG_REDUCE_GEN_SKEW", "1")
-    ds, b = _split_row_data(cfk, oracle_mod)
-    F = np.random.default_rng(2).random((len(b.user.ids), k)).astype(np.float32 if prec == "f32" else np.float64)
-    eng = _engine(cfk, k, prec, 0, ds.shard_block(0), len(b.user.ids), F)
-    st = eng.block_stats(0)
-    eng.solve_half(0, LAM)
-    from cfk_amd._lib import ALSError
-    with pytest.raises(ALSError, match="ALS_ERR_INTEGRITY"):
-        eng.read_factors(0)
-    rec = eng.integrity_status(reset=True)
-    # every REDUCE task fails (the record counts failing REDUCE tasks)
-    n_slots = st["n_tasks"] - (len(b.movie.ids) - st["n_reduce"])
-    assert rec[0] == st["n_reduce"], (rec, st)
-    assert rec[2] < n_slots and rec[3] < len(b.movie.ids)
-    assert eng.integrity_status() == [0, 0, 0, 0]
-    eng.read_factors(0)   # cleared: synchronising calls succeed again
-    eng.close()
+    caught, reported with its slot and row, and cleared by a reset. The knob exists only in the debug build
+    (CFK_DEBUG_KNOBS), so the cases run in a child process on build_debug/libcfk_als.so
+    (tests/integrity_fault_injection.py); the product library cannot be told to skew."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = dict(os.environ, ALS_CHUNK="64", ALS_DEBUG_REDUCE_GEN_SKEW="1",
+               CFK_ALS_LIB=os.path.join(ROOT, "collaborative-filtering-kafka_amd", "build_debug", "libcfk_als.so"))
+    res = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "integrity_fault_injection.py")],
+                         env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-3000:]
+    cases = [json.loads(line) for line in res.stdout.splitlines() if line.startswith("{")]
+    assert len(cases) == 4, res.stdout
+    for c in cases:
+        st, rec = c["stats"], c["rec"]
+        assert c["raised"] and "ALS_ERR_INTEGRITY" in c["raised"], c
+        # every REDUCE task fails (the record counts failing REDUCE tasks)
+        n_slots = st["n_tasks"] - (c["n_movies"] - st["n_reduce"])
+        assert rec[0] == st["n_reduce"] > 0, c
+        assert rec[2] < n_slots and rec[3] < c["n_movies"], c
+        assert c["after"] == [0, 0, 0, 0], c
+
+
+def test_product_library_has_no_debug_knobs():
+    """The work-dropping and integrity-weakening knobs compile into the debug build only."""
+    import os
+    from conftest import ROOT
+    blob = open(os.path.join(ROOT, "collaborative-filtering-kafka_amd", "build", "libcfk_als.so"), "rb").read()
+    assert b"ALS_DEBUG_" not in blob
+    dbg = open(os.path.join(ROOT, "collaborative-filtering-kafka_amd", "build_debug", "libcfk_als.so"), "rb").read()
+    assert b"ALS_DEBUG_REDUCE_GEN_SKEW" in dbg and b"ALS_DEBUG_SKIP_SOLVE" in dbg
 
 
 def _check_vs_oracle(got32, ref, ref32):
@@ -97,9 +110,10 @@ def _check_vs_oracle(got32, ref, ref32):
 @pytest.mark.parametrize("k", [64, 128])
 @pytest.mark.parametrize("presplit_env", [None, "1", "0"])
 def test_extreme_short_ratings_every_path(cfk, oracle_mod, monkeypatch, k, presplit_env):
-    """Ratings from {-32768, -1, 0, 257, 32767} (257 and 32767 are not bf16 numbers): both halves at k = 64 and
-    128 against the fp64 oracle. The user half at k = 64 is the pre-split candidate (small movie table); the
-    engine must not feed these ratings to its bf16 RHS operand, even when ALS_PRESPLIT=1 asks for it."""
+    """Ratings from {-32768, -1, 0, 257, 32767} (257 and 32767 are neither bf16 nor fp16 numbers): both halves at
+    k = 64 and 128 against the fp64 oracle. The pre-split Gram (default at KP = 64 and 128) feeds them to its RHS
+    MFMAs as rh + rm fp16 pairs (exact for every Java short); ALS_PRESPLIT=0 takes the on-the-fly bf16 split with
+    its fp32 VALU RHS."""
     if presplit_env is not None:
         monkeypatch.setenv("ALS_PRESPLIT", presplit_env)
     ds, b = _split_row_data(cfk, oracle_mod, ratings=[-32768, -1, 0, 257, 32767], seed=5)
@@ -109,24 +123,29 @@ def test_extreme_short_ratings_every_path(cfk, oracle_mod, monkeypatch, k, presp
         ref = oracle_mod.update_side(rows, F, LAM, "f64")
         ref32 = oracle_mod.update_side(rows, F.astype(np.float32), LAM, "f32")
         eng = _engine(cfk, k, "f32", side, ds.shard_block(side), len(opp.ids), F.astype(np.float32))
-        assert not eng.block_path(side)["presplit"]          # |r| > 256: never the bf16 RHS operand
+        assert eng.block_path(side)["presplit"] == (presplit_env != "0")
         eng.solve_half(side, LAM)
         got = eng.read_factors(side)
         eng.close()
         _check_vs_oracle(got, ref, ref32)
 
 
-def test_presplit_path_with_bf16_exact_extreme_ratings(cfk, oracle_mod):
-    """Ratings in [-256, 256] are bf16 numbers: the pre-split user half (k = 64, small movie table) stays on its
-    MFMA RHS and must still be within the reference's fp32 envelope."""
-    ds, b = _split_row_data(cfk, oracle_mod, ratings=[-256, -255, -1, 0, 1, 255, 256], seed=6)
-    F = np.random.default_rng(9).random((len(b.movie.ids), 64))
-    ref = oracle_mod.update_side(b.user, F, LAM, "f64")
-    ref32 = oracle_mod.update_side(b.user, F.astype(np.float32), LAM, "f32")
-    eng = _engine(cfk, 64, "f32", 1, ds.shard_block(1), len(b.movie.ids), F.astype(np.float32))
-    bp = eng.block_path(1)
-    assert bp["gram_path"] == "mfma_split" and bp["presplit"]
-    eng.solve_half(1, LAM)
-    got = eng.read_factors(1)
-    eng.close()
-    _check_vs_oracle(got, ref, ref32)
+@pytest.mark.parametrize("scale", [1e-20, 1e-6, 1.0, 3e4, 1e12])
+def test_presplit_scale_extreme_factor_magnitudes(cfk, oracle_mod, scale):
+    """The fp16 pre-split scales each opposite table by 2^s from its largest |x| (als_absmax, split_exp): tables of
+    any magnitude whose Gram fits fp32 -- far below the fp16 range, far beyond its 65504 maximum -- stay within the fp32 envelope, both halves,
+    k = 64 and 128."""
+    ds, b = _split_row_data(cfk, oracle_mod, seed=7)
+    for k in (64, 128):
+        rng = np.random.default_rng(k)
+        for side, rows, opp in ((0, b.movie, b.user), (1, b.user, b.movie)):
+            F = rng.standard_normal((len(opp.ids), k)) * scale
+            ref = oracle_mod.update_side(rows, F, LAM, "f64")
+            ref32 = oracle_mod.update_side(rows, F.astype(np.float32), LAM, "f32")
+            eng = _engine(cfk, k, "f32", side, ds.shard_block(side), len(opp.ids), F.astype(np.float32))
+            assert eng.block_path(side)["presplit"]
+            eng.solve_half(side, LAM)
+            got = eng.read_factors(side)
+            eng.close()
+            assert np.all(np.isfinite(got))
+            _check_vs_oracle(got, ref, ref32)

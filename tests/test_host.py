@@ -142,6 +142,29 @@ def test_synthetic_powerlaw_generator(cfk):
     assert deg.min() >= 1 and deg.max() > 20 * np.median(deg)
 
 
+@pytest.mark.parametrize("workload", ["powerlaw", "netflix"])
+def test_shard_restricted_synthesis_equals_the_full_dataset(cfk, workload):
+    """One process of the G-GPU bench holds only its shard's ratings (als_dataset_synthetic_*_shard): every query
+    the sharded driver makes for its shard -- both sides' COO in-blocks, shard geometry, slot layout (chunked too),
+    U0 -- equals the full dataset's."""
+    nu, nm, nnz, G = 20_000, 1_500, 600_000, 3
+    full = (cfk.Dataset.synthetic_powerlaw if workload == "powerlaw" else cfk.Dataset.synthetic_netflix)(
+        nu, nm, nnz, 5, 4)
+    full.set_slot_chunks(1, 2)
+    u0 = full.init_user_factors(16, 42, G)
+    for shard in range(G):
+        part = cfk.Dataset.synthetic_shard(workload, nu, nm, nnz, 5, G, shard, nthreads=3)
+        part.set_slot_chunks(1, 2)
+        assert part.counts()[:2] == (nm, nu) and part.counts()[2] < nnz
+        for side in (0, 1):
+            assert part.shard_info(side, G, shard) == full.shard_info(side, G, shard)
+            assert part.slot_layout(side, G) == full.slot_layout(side, G)
+            a, b = part.shard_coo(side, G, shard), full.shard_coo(side, G, shard)
+            for key in ("rows", "cols", "ratings"):
+                assert np.array_equal(a[key], b[key]), (shard, side, key)
+        assert np.array_equal(part.init_user_factors(16, 42, G), u0)
+
+
 def test_synthetic_generator_shape(cfk):
     ds = cfk.Dataset.synthetic_netflix(n_users=20_000, n_movies=2_000, nnz=400_000, seed=5, nthreads=4)
     nm, nu, nnz = ds.counts()

@@ -2,8 +2,8 @@
 reference's Java 13), the Panama FFM binding (AlsFfm.java, Java 22+), the re-plumbed processors and the topology
 under integration/java.
 
-There is no JDK in this image, so neither the Java nor the JNI shim (it needs jni.h) is compiled here. What is
-checked (CPU only):
+There is no JDK in this image, so the Java side is not compiled here; the JNI shim IS compiled and executed against a
+test-only jni.h and a mock JVM (tests/jni, tests/test_jni_shim.py). What is checked here (CPU only, on the sources):
 - every downcall descriptor in AlsFfm.java matches the C prototype: the library's ctypes signatures
   (_lib.SIGNATURES, themselves checked against the exports in test_host.py), int -> JAVA_INT,
   int64_t -> JAVA_LONG, float -> JAVA_FLOAT, pointers -> ADDRESS;
@@ -39,7 +39,7 @@ JNI_C = os.path.join(ROOT, "integration", "jni", "cfk_als_jni.c")
 JNI_PREFIX = "Java_de_hpi_collaborativefilteringkafka_nativeals_AlsNative_"
 JNI_TYPES = {"int": "jint", "long": "jlong", "float": "jfloat", "void": "void", "short": "jshort",
              "int[]": "jintArray", "long[]": "jlongArray", "float[]": "jfloatArray", "short[]": "jshortArray",
-             "byte[]": "jbyteArray", "String": "jstring"}
+             "byte[]": "jbyteArray", "double[]": "jdoubleArray", "String": "jstring"}
 
 
 def _ffm_layout(ct) -> str:

@@ -8,7 +8,7 @@ llvm-objdump --mcpu=gfx950):
   1. the kernels are built with -fno-slp-vectorize (csrc/Makefile): no v_pk_{add,mul,fma}_f32 in any als_solve_*
      kernel;
   2. every split-Gram MFMA group ends with MFMA_DRAIN (two `s_nop 7`, als_kernels.hip): after each
-     v_mfma_f32_16x16x32_bf16, no instruction writes its SrcA or SrcB registers -- which LLVM models as read at
+     v_mfma_f32_16x16x32_bf16 / _f16, no instruction writes its SrcA or SrcB registers -- which LLVM models as read at
      issue -- before that drain, and no branch leaves before it. SrcC, when it is not the MFMA's own destination
      (an accumulator the register allocator moves, KP = 128), is not checked: the compiler's hazard recognizer
      models that WAR and pads it itself (e.g. `s_nop 4` before the v_accvgpr_write of a source accumulator).
@@ -92,7 +92,7 @@ def test_every_split_gram_mfma_is_drained_before_its_operands_change(kernels):
     checked, violations = 0, []
     for name, ins in _solve_kernels(kernels).items():
         for i, (op, ops) in enumerate(ins):
-            if op != "v_mfma_f32_16x16x32_bf16":
+            if op not in ("v_mfma_f32_16x16x32_bf16", "v_mfma_f32_16x16x32_f16"):
                 continue
             checked += 1
             dst = _regs(ops[0])
@@ -116,3 +116,25 @@ def test_every_split_gram_mfma_is_drained_before_its_operands_change(kernels):
                 violations.append((name, i, "no MFMA_DRAIN before a branch / the end", ""))
     assert checked > 100, checked
     assert not violations, violations[:8]
+
+
+def test_lds_dma_image_waited_before_transposed_reads(kernels):
+    """Pre-split Gram: every ds_read_b64_tr_b16 of the LDS image has an `s_waitcnt vmcnt` between it and the
+    preceding global_load_lds_dwordx4 that fills the image (the explicit wait in als_kernels.hip): nothing orders a
+    ds_read behind a pending LDS-DMA but that wait (MI355X_MICROARCH.md, "Two waves per SIMD" item 7)."""
+    checked, bad = 0, []
+    for name, ins in _solve_kernels(kernels).items():
+        if not any(op == "global_load_lds_dwordx4" for op, _ in ins):
+            continue
+        last_dma, waited = None, True
+        for i, (op, ops) in enumerate(ins):
+            if op == "global_load_lds_dwordx4":
+                last_dma, waited = i, False
+            elif op == "s_waitcnt" and any(o.startswith("vmcnt") for o in " ".join(ops).split()):
+                waited = True
+            elif op == "ds_read_b64_tr_b16":
+                checked += 1
+                if last_dma is not None and not waited:
+                    bad.append((name, i, last_dma))
+    assert checked >= 32, checked
+    assert not bad, bad[:8]

@@ -9,7 +9,8 @@ Writes:
                               KiB -> B, FETCH doubled on gfx950), and the SQ counters of the full launch and of
                               the Gram alone (ALS_DEBUG_SKIP_SOLVE=1): MFMA busy share, issue stalls, clock
   bench_line.json             the bench.py line of the same call
-and profiles/counters_k<k>.json (read by bench.py): per side the HBM bytes per launch, the MFMA-pipe busy share of
+and profiles/counters_k<k>.json (read by bench.py, which uses it only when its lib_sha256 -- the library the profiled
+bench line reports -- is the library it runs): per side the HBM bytes per launch, the MFMA-pipe busy share of
 the whole launch and of the Gram alone (debug build, ALS_DEBUG_SKIP_SOLVE=1), the sustained clock, and the solve
 phase = whole launch minus Gram-only counters (its share of the launch's cycles, MFMA busy and VALU issue share).
 Sides: the main solve kernel dispatch with the largest grid is the user half (480,189 tasks), the next the movie
@@ -158,6 +159,7 @@ def main(tag, name):
             d["lds"] = {x: ld[x] for x in ("lds_bank_conflict_frac", "lds_active_frac", "wait_inst_lds_frac") if x in ld}
         per_side[side] = d
     json.dump({"k": k, "nnz": cfg.get("nnz", 100_000_000), "per_side": per_side, "source": f"profiles/{name}",
+               "lib_sha256": bench.get("build", {}).get("lib_sha256"),
                "note": "per launch; hbm_bytes = FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> B (Infinity-Cache "
                        "hits are counted by these counters); *_frac over 1024 SIMDs x the launch's GPU cycles "
                        "(GRBM_GUI_ACTIVE / 8 XCDs)"},

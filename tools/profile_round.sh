@@ -27,7 +27,7 @@ step 300 bench.json python3 bench.py $*
 step 300 trace.log rocprofv3 --kernel-trace --stats -d "$O/trace" -o run --output-format csv -- python3 "$R/bench.py" $B
 step 300 fetch.log rocprofv3 --pmc FETCH_SIZE -d "$O/fetch" -o run --output-format csv -- python3 "$R/bench.py" $P
 step 300 write.log rocprofv3 --pmc WRITE_SIZE -d "$O/write" -o run --output-format csv -- python3 "$R/bench.py" $P
-SQ="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE"
+SQ="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE"
 step 300 sq.log rocprofv3 --pmc $SQ -d "$O/sq" -o run --output-format csv -- python3 "$R/bench.py" $P
 CFK_ALS_LIB=$R/collaborative-filtering-kafka_amd/build_debug/libcfk_als.so ALS_DEBUG_SKIP_SOLVE=1 \
     step 300 sq_gram.log rocprofv3 --pmc $SQ -d "$O/sq_gram" -o run --output-format csv -- python3 "$R/bench.py" $P
