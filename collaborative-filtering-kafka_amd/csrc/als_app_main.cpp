@@ -72,9 +72,9 @@ int main(int argc, char** argv) {
         return 0;
     }
     long long P, K, N, NM, NU;
-    if (!parse_int(argv[1], 1, INT_MAX, P) || !parse_int(argv[2], 1, 128, K) || !parse_int(argv[4], 0, INT_MAX, N) ||
+    if (!parse_int(argv[1], 1, INT_MAX, P) || !parse_int(argv[2], 1, 1024, K) || !parse_int(argv[4], 0, INT_MAX, N) ||
         !parse_int(argv[6], 0, INT_MAX, NM) || !parse_int(argv[7], 0, INT_MAX, NU)) {
-        fprintf(stderr, "als_app: bad integer argument (NUM_FEATURES must be 1..128; 1..64 with --precision f64)\n");
+        fprintf(stderr, "als_app: bad integer argument (NUM_FEATURES must be 1..1024)\n");
         return 1;
     }
     char* end = nullptr;

@@ -102,6 +102,7 @@ struct als_engine {
     Factors fac[2];
     void* d_partials = nullptr;
     size_t partial_bytes = 0;
+    int64_t generic_slabs = 0;      // generic path: Gram slabs in d_partials
     void* d_split = nullptr;        // pre-split opposite table (cfk::launch_presplit), sized for the larger need
     size_t split_bytes = 0;
     uint32_t* d_amax = nullptr;     // bits of the pre-split table's largest |x| (cfk::launch_absmax): its scale
@@ -229,19 +230,23 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
     if (precision != ALS_F32 && precision != ALS_F64)
         return fail(ALS_ERR_INVALID_ARGUMENT, "precision must be ALS_F32 or ALS_F64");
     if (num_features < 1) return fail(ALS_ERR_INVALID_ARGUMENT, "num_features must be >= 1, got %d", num_features);
+    // padded row stride: 16 / 32 / 64 / 128 for the wave-per-row kernels, beyond them (fp32 k > 128, fp64 k > 64:
+    // the generic workgroup-per-row path) the next multiple of 16; the reference accepts any NUM_FEATURES
+    // (ALSAppRunner.java:18), this build up to 1024
+    if (num_features > 1024)
+        return fail(ALS_ERR_UNSUPPORTED, "num_features=%d: this build supports 1..1024", num_features);
+    const bool generic = num_features > (precision == ALS_F64 ? 64 : 128);
     int kp = num_features <= 16 ? 16 : num_features <= 32 ? 32 : num_features <= 64 ? 64 : 128;
-    if (num_features > 128 || (precision == ALS_F64 && num_features > 64))
-        return fail(ALS_ERR_UNSUPPORTED, "num_features=%d: this build supports 1..128 (f32) / 1..64 (f64)",
-                    num_features);
+    if (generic) kp = (num_features + 15) / 16 * 16;
     // MFMA Gram only where the accumulation is a real dense contraction (k >= 32, north star); fp64 and
-    // small k use the LDS-staged VALU Gram. fp32 Gram products via the exact three-term bf16 split (Path::MFMA_SPLIT) by default;
+    // small k use the LDS-staged VALU Gram. fp32 Gram products via the exact split (Path::MFMA_SPLIT) by default;
     // ALS_GRAM=f32 selects the v_mfma_f32_16x16x4_f32 path (same accumulator layout, 2.3x the Gram time).
-    Path path = (precision == ALS_F32 && num_features >= 32) ? Path::MFMA_SPLIT : Path::VALU;
+    Path path = generic ? Path::GENERIC : (precision == ALS_F32 && num_features >= 32) ? Path::MFMA_SPLIT : Path::VALU;
     if (path == Path::MFMA_SPLIT)
         if (const char* env = getenv("ALS_GRAM"))
             if (!strcmp(env, "f32")) path = Path::MFMA;
     if (const char* env = getenv("ALS_FORCE_VALU"))
-        if (env[0] == '1') path = Path::VALU;
+        if (env[0] == '1' && !generic) path = Path::VALU;
     if (!cfk::variant_available(precision, kp, path))
         return fail(ALS_ERR_UNSUPPORTED, "no kernel variant for precision=%d kp=%d", precision, kp);
     int ndev = 0;
@@ -395,7 +400,8 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
         (void)hipFree(d_col);
         (void)hipFree(d_rat);
     };
-    const int64_t chunk = chunk_entries(nnz_padded);
+    // the generic path's workgroup takes a whole row of any length: no split rows
+    const int64_t chunk = e->path == Path::GENERIC ? INT64_MAX : chunk_entries(nnz_padded);
     std::vector<Task> tasks, reduce;
     int64_t slots = 0;
     for (int64_t i = 0; i < n_rows; ++i) {
@@ -480,14 +486,17 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     blk.n_tasks = (int32_t)tasks.size();
     blk.n_reduce = (int32_t)reduce.size();
     blk.n_slots = (int32_t)slots;
-    // Pre-split opposite table (scaled two-term fp16, cfk::launch_presplit, once per half) for the MFMA Gram at KP = 64
-    // and 128: 4 KP bytes per row (the fp32 row's size), 3 MFMAs per tile instead of the on-the-fly bf16 split's 6,
-    // no split VALU (the rows reach LDS by DMA and the MFMA operands come back with transposed reads).
-    // ALS_PRESPLIT=0/1 forces it off/on.
+    // Pre-split opposite table (scaled two-term fp16, cfk::launch_presplit, once per half) for the MFMA Gram: 4 KP
+    // bytes per row (the fp32 row's size), 3 MFMAs per tile instead of the on-the-fly bf16 split's 6, no split VALU
+    // (the rows reach LDS by DMA and the MFMA operands come back with transposed reads). Chosen where the Gram is
+    // MFMA-bound: always at KP = 128, and at KP = 64 for a cache-resident opposite table (<= 8 MB: the 17,770-row
+    // movie table of the user half, 2.99 vs 4.37 ms). The KP = 64 movie half gathers the 123 MB user table at the
+    // Infinity-Cache ceiling either way, and the split pass over that table would cost more than it saves (3.08 vs
+    // 3.01 ms; kbench). ALS_PRESPLIT=0/1 forces it off/on.
     {
         const int64_t sb = (n_opp_rows + 1) * (int64_t)cfk::presplit_row_bytes(e->kp);
         const bool ps_kp = e->path == Path::MFMA_SPLIT && (e->kp == 64 || e->kp == 128);
-        bool ps = ps_kp;
+        bool ps = ps_kp && (e->kp == 128 || sb <= (8ll << 20));
         if (const char* env = getenv("ALS_PRESPLIT")) ps = ps_kp && env[0] == '1';
         // the pre-split gather forms 32-bit byte offsets row * presplit_row_bytes with a 24-bit multiply: both the
         // row (< 2^24) and the offset (< 2^32) must fit, also when ALS_PRESPLIT=1 forces the path
@@ -539,8 +548,17 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     if (!sq_all.empty()) HIP_TRY(hipMalloc((void**)&blk.d_task_se, sq_all.size() * sizeof(double)));
     blk.h_tasks = std::move(tasks);
     blk.h_reduce = std::move(reduce);
-    // Partial workspace sized for the larger side.
-    const size_t need = (size_t)slots * cfk::partial_words_per_lane(e->precision, e->kp, e->path) * 64 * e->elem();
+    // Partial workspace sized for the larger side (the generic path: its per-workgroup Gram slabs, when the packed
+    // triangle does not fit in LDS -- up to 1024 workgroups within 4 GiB)
+    size_t need = (size_t)slots * cfk::partial_words_per_lane(e->precision, e->kp, e->path) * 64 * e->elem();
+    if (e->path == Path::GENERIC) {
+        const cfk::GenericPlan gp = cfk::generic_plan(e->precision, e->kp);
+        if (!gp.g_in_lds) {
+            const int64_t slab = gp.slab_elems * (int64_t)e->elem();
+            e->generic_slabs = std::max<int64_t>(1, std::min<int64_t>(1024, (4ll << 30) / slab));
+            need = (size_t)(e->generic_slabs * slab);
+        }
+    }
     if (need > e->partial_bytes) {
         (void)hipFree(e->d_partials);
         e->d_partials = nullptr;
@@ -774,6 +792,7 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
     a.rows_per_chunk = (int32_t)b.rows_per_chunk;
     a.chunk_stride = b.chunk_stride;
     a.partials = e->d_partials;
+    a.scratch_slabs = e->generic_slabs;
     a.lambda = lambda;
     a.sentinel = (int32_t)b.n_opp_rows;
     a.flags = e->path == Path::VALU ? 0 : e->debug_flags;

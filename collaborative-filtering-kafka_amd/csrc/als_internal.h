@@ -67,6 +67,7 @@ struct SolveArgs {
     int64_t chunk_stride;   //   row_offset + (row / rows_per_chunk) * chunk_stride + row % rows_per_chunk
     int64_t rat_lo_off;     // presplit: words from the rh pairs to the rm pairs (nnz_padded / 2)
     const uint32_t* amax;   // presplit: bits of the opposite table's largest |x| (als_absmax): the split scale
+    int64_t scratch_slabs;  // generic path: workgroup slabs in `partials` (its Gram when it does not fit in LDS)
 };
 // Factor row of local row `row` under the block's slot layout (wave-uniform: scalar arithmetic, once per task).
 __host__ __device__ inline int64_t factor_row(int64_t row_offset, int32_t rows_per_chunk, int64_t chunk_stride,
@@ -102,7 +103,18 @@ struct SqErrArgs {
 // products), MFMA_SPLIT (fp32 operands split into narrow terms, fp32 accumulation: fp32-accurate products at a
 // multiple of the f32 MFMA rate): on the fly into three bf16 terms (six v_mfma_f32_16x16x32_bf16 partial products
 // per tile), or -- presplit -- once per half into a scaled two-term fp16 table (three v_mfma_f32_16x16x32_f16).
-enum class Path : int { VALU = 0, MFMA = 1, MFMA_SPLIT = 2 };
+// GENERIC: any num_features beyond the wave-per-row kernels (fp32 k > 128, fp64 k > 64): one workgroup per row,
+// the Gram's packed lower triangle in LDS (or a per-workgroup global slab) and a workgroup Cholesky.
+enum class Path : int { VALU = 0, MFMA = 1, MFMA_SPLIT = 2, GENERIC = 3 };
+// Launch geometry of the generic path for (precision, kp): LDS or slab Gram, staged rows per batch, dynamic LDS.
+struct GenericPlan {
+    bool g_in_lds;
+    int batch;
+    int64_t lds_bytes;
+    int64_t slab_elems;   // elements per workgroup slab of SolveArgs::partials (0 when the Gram is in LDS)
+};
+GenericPlan generic_plan(int precision, int kp);
+hipError_t launch_generic(int precision, int kp, const SolveArgs& a, hipStream_t s);
 
 // Launch helpers (defined in als_kernels.hip). Return hipSuccess or the launch error.
 // min_waves: occupancy target (waves per SIMD) of the MFMA variant (__launch_bounds__ second argument).

@@ -536,24 +536,84 @@ __device__ __forceinline__ float row_sum_to_last(float v) {
 // a[i][p] + a[i][p] (d - 1)(-1/d) = a[i][p] / d. That FMA is accurate to a few ulp only while d <= 1,
 // which the caller guarantees by Jacobi-scaling the system to a unit diagonal (every later pivot is a
 // Schur-complement diagonal of a unit-diagonal SPD matrix, so it stays in (0, 1]).
+template <bool SWAP, int p>
+__device__ __forceinline__ void sweep_step(f32x4& a, int lane, float& nrd_min) {
+    constexpr int pg = p >> 2, pr = p & 3;
+    const float nrd = __builtin_amdgcn_rcpf(-bcast(a[pr], 16 * pg + p));   // -1 / d
+    nrd_min = fminf(nrd_min, nrd);                                          // -1 / (smallest pivot)
+    const bool piv = lane == 16 * pg + p;   // 16 lane masks, CSE-d across the 4 diagonal tiles (SGPRs)
+    a[pr] = piv ? a[pr] - 1.f : a[pr];
+    const float t = (SWAP ? col_bcast_swap<pg>(a[pr]) : col_bcast<pg>(a[pr])) * nrd;   // a[p][c] (d - 1 at c = p) * (-1/d)
+    f32x4 cp;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cp[r] = row_lane_bcast<p>(a[r]);   // a[4g + r][p] (d - 1 at row p)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a[r] += cp[r] * t;
+    a[pr] = piv ? nrd : a[pr];
+}
 template <bool SWAP>
 __device__ __forceinline__ void sweep_tile(f32x4& a, int lane, float& nrd_min) {
-    static_for<0, 16>([&](auto P_) {
-        constexpr int p = decltype(P_)::value;
-        constexpr int pg = p >> 2, pr = p & 3;
-        const float nrd = __builtin_amdgcn_rcpf(-bcast(a[pr], 16 * pg + p));   // -1 / d
-        nrd_min = fminf(nrd_min, nrd);                                          // -1 / (smallest pivot)
-        const bool piv = lane == 16 * pg + p;   // 16 lane masks, CSE-d across the 4 diagonal tiles (SGPRs)
-        a[pr] = piv ? a[pr] - 1.f : a[pr];
-        const float t = (SWAP ? col_bcast_swap<pg>(a[pr]) : col_bcast<pg>(a[pr])) * nrd;   // a[p][c] (d - 1 at c = p) * (-1/d)
-        f32x4 cp;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cp[r] = row_lane_bcast<p>(a[r]);   // a[4g + r][p] (d - 1 at row p)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) a[r] += cp[r] * t;
-        a[pr] = piv ? nrd : a[pr];
-    });
+    static_for<0, 16>([&](auto P_) { sweep_step<SWAP, decltype(P_)::value>(a, lane, nrd_min); });
 }
+
+// D + X^T Y of two 16 x 16 tiles in accumulator layout (the solve's block products): four v_mfma_f32_16x16x4_f32
+// (exact fp32 products, 128 MFMA cycles), or -- CFK_SOLVE_SPLIT -- both operands split exactly into three bf16 terms
+// (split3) and the six partial products hh, mh, hm, mm, hl, lh in three v_mfma_f32_16x16x32_bf16 (48 cycles): lane
+// (g, c)'s eight k slots of the 16x16x32 operand are its four rows 4g + r of column c in two terms, so X^T Y needs no
+// lane movement; each bf16 product is exact in fp32 and the dropped ml, lm, ll terms are below 2^-26 |xy|.
+#ifndef CFK_SOLVE_SPLIT
+#define CFK_SOLVE_SPLIT 0
+#endif
+__device__ __forceinline__ f32x4 tile_tn(const f32x4& X, const f32x4& Y, f32x4 D) {
+    if constexpr (CFK_SOLVE_SPLIT) {
+        unsigned xh0, xm0, xl0, xh1, xm1, xl1, yh0, ym0, yl0, yh1, ym1, yl1;
+        split3(X[0], X[1], xh0, xm0, xl0);
+        split3(X[2], X[3], xh1, xm1, xl1);
+        split3(Y[0], Y[1], yh0, ym0, yl0);
+        split3(Y[2], Y[3], yh1, ym1, yl1);
+        const u32x4 ahl = {xh0, xh1, xl0, xl1}, ahm = {xh0, xh1, xm0, xm1};
+        const u32x4 blh = {yl0, yl1, yh0, yh1}, bmm = {ym0, ym1, ym0, ym1}, bhh = {yh0, yh1, yh0, yh1};
+        __builtin_amdgcn_sched_barrier(0);
+        D = mfma_k32(ahl, blh, D);   // hl + lh
+        D = mfma_k32(ahm, bmm, D);   // hm + mm
+        D = mfma_k32(ahm, bhh, D);   // hh + mh
+        MFMA_DRAIN();
+        asm volatile("" ::"v"(ahl), "v"(ahm), "v"(blh), "v"(bmm), "v"(bhh));   // operands live past the drain
+        return D;
+    } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) D = __builtin_amdgcn_mfma_f32_16x16x4f32(X[s], Y[s], D, 0, 0, 0);
+        return D;
+    }
+}
+
+// Lookahead schedule of the block factorisation (CFK_SOLVE_LOOKAHEAD): step P first finishes block column P + 1
+// (V'_{P,P+1} and the update of T_{P+1,P+1}), so the 16-step sweep of T_{P+1,P+1} -- a dependent chain of
+// broadcasts, latency-bound -- can start at once, and the rest of step P's MFMA work (block columns J >= P + 2) is
+// issued between its steps. Items of step P, J descending, per J: V'_PJ = S_P T_PJ, then T_IJ += T_PI^T V'_PJ for
+// I = P + 1 .. J (the same single update per tile as the plain order: bitwise equal results).
+__host__ __device__ constexpr int la_items(int C, int P) {
+    int n = 0;
+    for (int J = C - 1; J >= P + 2; --J) n += 1 + (J - P);
+    return n;
+}
+__host__ __device__ constexpr int la_item_J(int C, int P, int t) {
+    for (int J = C - 1; J >= P + 2; --J) {
+        if (t < 1 + J - P) return J;
+        t -= 1 + J - P;
+    }
+    return -1;
+}
+__host__ __device__ constexpr int la_item_I(int C, int P, int t) {   // -1: the V'_PJ item of its J
+    for (int J = C - 1; J >= P + 2; --J) {
+        if (t < 1 + J - P) return t == 0 ? -1 : P + t;
+        t -= 1 + J - P;
+    }
+    return -2;
+}
+#ifndef CFK_SOLVE_LOOKAHEAD
+#define CFK_SOLVE_LOOKAHEAD 1
+#endif
 
 // Block LDL^T solve on the Gram tiles left in the MFMA accumulators (no LDS copy of the matrix).
 // With C = KP/16 the accumulators hold G' = P G P^T (feature f = C*i + b at position 16*b + i) as upper
@@ -700,10 +760,48 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 
     // ---- factorisation (matrix part only) ----
     float nrd_min = -1.f;
+    constexpr bool SWAPC = 16 * C >= CFK_COL_SWAP;
+    if constexpr (CFK_SOLVE_LOOKAHEAD) {
+        {
+            f32x4 S0 = T.get(tile_index<C>(0, 0));
+            sweep_tile<SWAPC>(S0, lane, nrd_min);
+            T.put(tile_index<C>(0, 0), S0);
+        }
+        static_for<0, C - 1>([&](auto P_) {
+            constexpr int P = decltype(P_)::value;
+            const f32x4 S = T.get(tile_index<C>(P, P));   // -T_PP^{-1}
+            const f32x4 orig = T.get(tile_index<C>(P, P + 1));
+            const f32x4 v1 = tile_tn(S, orig, f32x4{0.f, 0.f, 0.f, 0.f});
+            f32x4 D = tile_tn(orig, v1, T.get(tile_index<C>(P + 1, P + 1)));
+            T.put(tile_index<C>(P, P + 1), v1);
+            constexpr int m = la_items(C, P);
+            f32x4 vcur = {0.f, 0.f, 0.f, 0.f};
+            auto item = [&](auto T_) {
+                constexpr int t = decltype(T_)::value;
+                constexpr int J = la_item_J(C, P, t), I = la_item_I(C, P, t);
+                if constexpr (I < 0) {
+                    vcur = tile_tn(S, T.get(tile_index<C>(P, J)), f32x4{0.f, 0.f, 0.f, 0.f});
+                } else {
+                    // T_PI: I = P + 1 was replaced by V'_{P,P+1} above (orig keeps it); P + 1 < I <= J is still the
+                    // original (replaced only when its own, later, J group ends)
+                    const f32x4 TPI = (I == P + 1) ? orig : T.get(tile_index<C>(P, I));
+                    T.put(tile_index<C>(I, J), tile_tn(TPI, vcur, T.get(tile_index<C>(I, J))));
+                    if constexpr (I == J) T.put(tile_index<C>(P, J), vcur);   // block row P now holds V'_PJ
+                }
+            };
+            // the sweep of T_{P+1,P+1} with step P's remaining items between its 16 pivot steps
+            static_for<0, 16>([&](auto Q_) {
+                constexpr int q = decltype(Q_)::value;
+                sweep_step<SWAPC, q>(D, lane, nrd_min);
+                static_for<q * m / 16, (q + 1) * m / 16>(item);
+            });
+            T.put(tile_index<C>(P + 1, P + 1), D);
+        });
+    } else
     static_for<0, C>([&](auto P_) {
         constexpr int P = decltype(P_)::value;
         f32x4 S = T.get(tile_index<C>(P, P));
-        sweep_tile<(16 * C >= CFK_COL_SWAP)>(S, lane, nrd_min);
+        sweep_tile<SWAPC>(S, lane, nrd_min);
         T.put(tile_index<C>(P, P), S);
         // Block columns J in DESCENDING order: V'_PJ only updates T_IJ (P < I <= J) from the still-unreplaced
         // T_PI (I <= J), so block row P can take V'_PJ right away and one V is live at a time. Every T_IJ
@@ -1833,6 +1931,150 @@ __global__ __launch_bounds__(256) void als_predict_kernel(const T* __restrict__ 
     out[u * n_m + m] = total;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Generic path: any num_features beyond the wave-per-row kernels (fp32 k > 128, fp64 k > 64)
+// ---------------------------------------------------------------------------------------------------
+// One 256-thread workgroup per row (FULL tasks only: the work plan never splits a row on this path), grid-stride
+// over the rows. MFeatureCalculator.java:85-99 for that row: the Gram's lower triangle and the RHS accumulated over
+// LDS-staged batches of gathered factor rows, A + lambda n I (padded features: identity), a right-looking Cholesky
+// (one pivot column per step, the trailing update spread over the workgroup), forward and backward substitution.
+// G_LDS: the packed lower triangle lives in LDS (kp <= 256 fp32, <= 128 fp64); otherwise in a per-workgroup slab
+// of `scratch` (slab elements each). Not a benchmark configuration: correctness for every k (ALSAppRunner.java:18
+// accepts any NUM_FEATURES), at the cost of O(k^2) LDS traffic per gathered row.
+template <class T, bool G_LDS>
+__global__ __launch_bounds__(256) void als_solve_generic(SolveArgs a, int kp, int batch, T* __restrict__ scratch,
+                                                         int64_t slab) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char gsmem[];
+    const int tid = threadIdx.x;
+    const int64_t ntri = (int64_t)kp * (kp + 1) / 2;
+    T* G = G_LDS ? (T*)gsmem : scratch + (int64_t)blockIdx.x * slab;   // packed lower triangle, tri(i, j)
+    T* stage = (T*)gsmem + (G_LDS ? ((ntri + 1) & ~(int64_t)1) : 0); // batch x kp gathered rows
+    __shared__ T vec[1024 + 1];                                         // RHS / solution (kp <= 1024) + pivot
+    const T* opp = (const T*)a.opp;
+    auto tri_ = [](int64_t i, int64_t j) { return i * (i + 1) / 2 + j; };
+    for (int task = blockIdx.x; task < a.n_tasks; task += gridDim.x) {
+        const Task tk = a.tasks[task];
+        T* out = (T*)a.out + factor_row(a.row_offset, a.rows_per_chunk, a.chunk_stride, tk.row) * (int64_t)kp;
+        for (int64_t x = tid; x < ntri; x += 256) G[x] = T(0);
+        for (int i = tid; i < kp; i += 256) vec[i] = T(0);
+        __syncthreads();
+        const int n = (tk.nsteps + BLOCK_SUBSTEPS - 1) / BLOCK_SUBSTEPS * BLOCK_ENTRIES;   // padded span
+        for (int base = 0; base < n; base += batch) {
+            const int nb = min(batch, n - base);
+            for (int x = tid; x < nb * kp; x += 256) {   // padding entries gather the zero sentinel row
+                const int e = x / kp, f = x - e * kp;
+                stage[x] = opp[(int64_t)a.col[tk.begin + base + e] * kp + f];
+            }
+            __syncthreads();
+            for (int i = tid; i < kp; i += 256) {
+                T acc = vec[i];
+                for (int e = 0; e < nb; ++e) acc += (T)a.rat[tk.begin + base + e] * stage[e * kp + i];
+                vec[i] = acc;
+            }
+            for (int64_t x = tid; x < ntri; x += 256) {
+                // row i of the packed triangle holding x: i (i + 1) / 2 <= x
+                int64_t i = (int64_t)((sqrt(8.0 * (double)x + 1.0) - 1.0) / 2.0);
+                while (i * (i + 1) / 2 > x) --i;
+                while ((i + 1) * (i + 2) / 2 <= x) ++i;
+                const int64_t j = x - i * (i + 1) / 2;
+                T acc = G[x];
+                for (int e = 0; e < nb; ++e) acc += stage[e * kp + i] * stage[e * kp + j];
+                G[x] = acc;
+            }
+            __syncthreads();
+        }
+        if (tk.ndeg == 0) {   // cannot occur in the reference; defined as 0 (as the other paths)
+            for (int i = tid; i < kp; i += 256) out[i] = T(0);
+            __syncthreads();
+            continue;
+        }
+        const T reg = (T)a.lambda * (T)tk.ndeg;   // A + lambda * (float) n on the diagonal (MFeatureCalculator.java:91-95)
+        for (int i = tid; i < kp; i += 256) {
+            const int64_t d = tri_(i, i);
+            G[d] = i < a.k ? G[d] + reg : T(1);
+        }
+        __syncthreads();
+        for (int j = 0; j < kp; ++j) {   // Cholesky: column j of L, then the trailing update
+            if (tid == 0) {
+                const T d = sqrt(G[tri_(j, j)]);
+                G[tri_(j, j)] = d;
+                vec[1024] = d;
+            }
+            __syncthreads();
+            const T d = vec[1024];
+            for (int i = j + 1 + tid; i < kp; i += 256) G[tri_(i, j)] /= d;
+            __syncthreads();
+            const int m = kp - j - 1;
+            for (int64_t x = tid; x < (int64_t)m * m; x += 256) {
+                const int i = j + 1 + (int)(x / m), l = j + 1 + (int)(x % m);
+                if (l <= i) G[tri_(i, l)] -= G[tri_(i, j)] * G[tri_(l, j)];
+            }
+            __syncthreads();
+        }
+        for (int j = 0; j < kp; ++j) {   // forward: L y = b (y over vec)
+            const T y = vec[j] / G[tri_(j, j)];
+            __syncthreads();
+            if (tid == 0) vec[j] = y;
+            for (int i = j + 1 + tid; i < kp; i += 256) vec[i] -= G[tri_(i, j)] * y;
+            __syncthreads();
+        }
+        for (int j = kp - 1; j >= 0; --j) {   // backward: L^T x = y
+            const T x = vec[j] / G[tri_(j, j)];
+            __syncthreads();
+            if (tid == 0) vec[j] = x;
+            for (int i = tid; i < j; i += 256) vec[i] -= G[tri_(j, i)] * x;
+            __syncthreads();
+        }
+        for (int i = tid; i < kp; i += 256) out[i] = i < a.k ? vec[i] : T(0);
+        __syncthreads();
+    }
+}
+
+// Squared error of the generic path (any kp): one wave per task, lane = feature stripe.
+template <class T>
+__global__ __launch_bounds__(256) void als_sq_error_generic(SqErrArgs a, int kp) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tid = blockIdx.x * WAVES + wave;
+    if (tid >= a.n_tasks) return;
+    const Task tk = load_task(a.tasks + tid);
+    const T* self = (const T*)a.self + factor_row(a.row_offset, a.rows_per_chunk, a.chunk_stride, tk.row) * (int64_t)kp;
+    const T* opp = (const T*)a.opp;
+    double se = 0.0;
+    const int n = (tk.nsteps + BLOCK_SUBSTEPS - 1) / BLOCK_SUBSTEPS * BLOCK_ENTRIES;
+    for (int e = 0; e < n; ++e) {
+        const int w = e % BLOCK_ENTRIES;
+        const int logical = e - w + (w % BLOCK_SUBSTEPS) * 4 + w / BLOCK_SUBSTEPS;
+        if (logical >= tk.nent) continue;   // wave-uniform
+        const T* y = opp + (int64_t)a.col[tk.begin + e] * kp;
+        T dot = T(0);
+        for (int f = lane; f < kp; f += 64) dot += self[f] * y[f];
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) dot += __shfl_xor(dot, m);
+        const double d = (double)a.rat[tk.begin + e] - (double)dot;
+        se += d * d;
+    }
+    if (lane == 0) a.task_se[tid] = se;
+}
+
+// Collector dot products for any k (FeatureCollector.java:90-101, Java-float order): one thread per cell.
+template <class T>
+__global__ __launch_bounds__(256) void als_predict_generic(const T* __restrict__ U, const T* __restrict__ M, int kp,
+                                                           int k, const int64_t* __restrict__ urows, int64_t n_u,
+                                                           const int64_t* __restrict__ mrows, int64_t n_m,
+                                                           float* __restrict__ out) {
+    const int64_t cell = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (cell >= n_u * n_m) return;
+    const int64_t u = cell / n_m, m = cell % n_m;
+    const T* x = U + urows[u] * kp;
+    const T* y = M + mrows[m] * kp;
+    float total = 0.f;
+    {
+#pragma clang fp contract(off)
+        for (int f = 0; f < k; ++f) total = total + (float)x[f] * (float)y[f];
+    }
+    out[cell] = total;
+}
+
 int blocks_for(int n_tasks) { return (n_tasks + WAVES - 1) / WAVES; }
 
 template <class T, int KP, Path P, int MINW = 1, bool PRESPLIT = false>
@@ -1870,6 +2112,7 @@ hipError_t launch_sq_t(const SqErrArgs& a, hipStream_t s) {
 }  // namespace
 
 bool variant_available(int precision, int kp, Path path) {
+    if (path == Path::GENERIC) return kp % 16 == 0 && kp <= 1024;
     if (precision == 0) {
         if (path == Path::MFMA || path == Path::MFMA_SPLIT) return kp == 32 || kp == 64 || kp == 128;
         return kp == 16 || kp == 32 || kp == 64;
@@ -1878,6 +2121,7 @@ bool variant_available(int precision, int kp, Path path) {
 }
 
 int partial_words_per_lane(int precision, int kp, Path path) {
+    if (path == Path::GENERIC) return 0;   // rows are never split on the generic path
     if (path == Path::MFMA || path == Path::MFMA_SPLIT) {
         const int c = kp / 16;
         return (c * (c + 1) / 2) * 4 + c + 1;   // accumulators + RHS + check word
@@ -1888,7 +2132,18 @@ int partial_words_per_lane(int precision, int kp, Path path) {
 hipError_t launch_predict(int precision, const void* U, const void* M, int kp, int k, const int64_t* urows,
                           int64_t n_u, const int64_t* mrows, int64_t n_m, float* out, hipStream_t s) {
     if (n_u <= 0 || n_m <= 0) return hipSuccess;
-    if (k > 128 || (n_m + 15) / 16 > INT32_MAX || (n_u + 15) / 16 > 65535) return hipErrorInvalidValue;
+    if (k > 128) {   // generic path: one thread per cell
+        const int64_t cells = n_u * n_m;
+        if ((cells + 255) / 256 > INT32_MAX) return hipErrorInvalidValue;
+        const unsigned g = (unsigned)((cells + 255) / 256);
+        if (precision == 0)
+            als_predict_generic<float><<<g, 256, 0, s>>>((const float*)U, (const float*)M, kp, k, urows, n_u, mrows, n_m, out);
+        else
+            als_predict_generic<double><<<g, 256, 0, s>>>((const double*)U, (const double*)M, kp, k, urows, n_u, mrows,
+                                                           n_m, out);
+        return hipGetLastError();
+    }
+    if ((n_m + 15) / 16 > INT32_MAX || (n_u + 15) / 16 > 65535) return hipErrorInvalidValue;
     const dim3 grid((unsigned)((n_m + 15) / 16), (unsigned)((n_u + 15) / 16));
     if (precision == 0)
         als_predict_kernel<float><<<grid, 256, 0, s>>>((const float*)U, (const float*)M, kp, k, urows, n_u, mrows, n_m, out);
@@ -1979,6 +2234,7 @@ hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s) {
 
 hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, int min_waves,
                         bool presplit, bool reduce) {
+    if (path == Path::GENERIC) return reduce ? hipErrorInvalidValue : launch_generic(precision, kp, a, s);
     if (precision == 0) {
         // occupancy (waves per SIMD) per variant: KP <= 64 two, the pre-split KP = 64 Gram three, KP = 128 one
         (void)min_waves;
@@ -2005,7 +2261,60 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
     return hipErrorInvalidValue;
 }
 
+GenericPlan generic_plan(int precision, int kp) {
+    GenericPlan p{};
+    const int64_t elem = precision == 0 ? 4 : 8;
+    const int64_t ntri = (int64_t)kp * (kp + 1) / 2;
+    const int64_t tri_b = ((ntri + 1) & ~(int64_t)1) * elem;
+    const int64_t avail = 160 * 1024 - 1025 * elem;   // LDS minus the kernel's static RHS vector
+    const int64_t row_b = (int64_t)kp * elem;
+    if (tri_b + 8 * row_b <= avail) {
+        p.g_in_lds = true;
+        p.batch = (int)std::min<int64_t>(64, (avail - tri_b) / row_b);
+        p.lds_bytes = tri_b + p.batch * row_b;
+        p.slab_elems = 0;
+    } else {
+        p.g_in_lds = false;
+        p.batch = (int)std::max<int64_t>(1, std::min<int64_t>(64, (64 * 1024) / row_b));
+        p.lds_bytes = p.batch * row_b;
+        p.slab_elems = ntri + 1;
+    }
+    return p;
+}
+
+template <class T, bool L>
+hipError_t launch_generic_t(const GenericPlan& p, int kp, const SolveArgs& a, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)als_solve_generic<T, L>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_bytes);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    int64_t grid = std::min<int64_t>(a.n_tasks, 4096);
+    if (!L) grid = std::min<int64_t>(grid, a.scratch_slabs);
+    if (grid <= 0) return hipErrorInvalidValue;
+    als_solve_generic<T, L><<<(unsigned)grid, 256, (size_t)p.lds_bytes, s>>>(a, kp, p.batch, (T*)a.partials,
+                                                                             p.slab_elems);
+    return hipGetLastError();
+}
+
+hipError_t launch_generic(int precision, int kp, const SolveArgs& a, hipStream_t s) {
+    if (a.n_tasks <= 0) return hipSuccess;
+    if (kp > 1024 || kp % 16) return hipErrorInvalidValue;
+    const GenericPlan p = generic_plan(precision, kp);
+    if (precision == 0)
+        return p.g_in_lds ? launch_generic_t<float, true>(p, kp, a, s) : launch_generic_t<float, false>(p, kp, a, s);
+    return p.g_in_lds ? launch_generic_t<double, true>(p, kp, a, s) : launch_generic_t<double, false>(p, kp, a, s);
+}
+
 hipError_t launch_sq_error(int precision, int kp, const SqErrArgs& a, hipStream_t s) {
+    if (kp > 128 || (precision == 1 && kp > 64)) {   // generic path
+        if (a.n_tasks <= 0) return hipSuccess;
+        if (precision == 0) als_sq_error_generic<float><<<blocks_for(a.n_tasks), 256, 0, s>>>(a, kp);
+        else als_sq_error_generic<double><<<blocks_for(a.n_tasks), 256, 0, s>>>(a, kp);
+        return hipGetLastError();
+    }
     if (precision == 0) {
         if (kp == 16) return launch_sq_t<float, 16>(a, s);
         if (kp == 32) return launch_sq_t<float, 32>(a, s);

@@ -27,7 +27,11 @@ def _side(s) -> int:
     return SIDES[s] if isinstance(s, str) else int(s)
 
 
-def factor_stride(k: int) -> int:
+def factor_stride(k: int, precision: str = "f32") -> int:
+    """Padded factor-row stride of an engine (als_factor_stride): 16 / 32 / 64 / 128 on the wave-per-row kernels,
+    the next multiple of 16 on the generic path (fp32 k > 128, fp64 k > 64)."""
+    if k > (64 if precision == "f64" else 128):
+        return (k + 15) // 16 * 16
     return 16 if k <= 16 else 32 if k <= 32 else 64 if k <= 64 else 128
 
 
@@ -435,7 +439,8 @@ class ALSEngine:
         """Gram variant of the side's block: gram_path ('valu' | 'mfma_f32' | 'mfma_split'), presplit, chunk."""
         g, p, c, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64(), (ctypes.c_int64 * 3)()
         call("als_block_path", self._h, _side(side), ctypes.byref(g), ctypes.byref(p), ctypes.byref(c), d)
-        return {"gram_path": ("valu", "mfma_f32", "mfma_split")[g.value], "presplit": bool(p.value), "chunk": c.value,
+        return {"gram_path": ("valu", "mfma_f32", "mfma_split", "generic")[g.value], "presplit": bool(p.value),
+                "chunk": c.value,
                 "dual_rows": sum(d), "dual_rows_by_blocks": list(d)}
 
     def block_stats(self, side):

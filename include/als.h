@@ -20,7 +20,7 @@
  *  - "side" selects the entity type whose rows are recomputed: ALS_SIDE_MOVIE rows are solved from user
  *    factors (MFeatureCalculator), ALS_SIDE_USER rows from movie factors (UFeatureCalculator).
  *  - Factor matrices live in device memory with a padded row stride (als_factor_stride(): 16, 32, 64 or
- *    128 elements); columns >= num_features are kept at zero by the engine.
+ *    128 elements, or num_features rounded up to 16 beyond that); columns >= num_features are kept at zero.
  */
 #ifndef CFK_ALS_H
 #define CFK_ALS_H
@@ -60,7 +60,8 @@ int         als_device_count(int* n);
 
 /* ---- engine lifetime ---------------------------------------------------------------------------- */
 /* Replaces the per-task processor state of MFeatureCalculator/UFeatureCalculator.init (:29-46).
- * num_features = ALSApp.NUM_FEATURES (ALSApp.java:18), 1..128 (f64: 1..64). */
+ * num_features = ALSApp.NUM_FEATURES (ALSApp.java:18), 1..1024: up to 128 (f64: 64) on the wave-per-row kernels,
+ * beyond that on the generic workgroup-per-row path (ALSAppRunner.java:18 accepts any value). */
 int als_engine_create(int device, int num_features, int precision, als_engine** out);
 int als_engine_destroy(als_engine* e);
 /* Launch on a caller-provided hipStream_t (e.g. torch's current stream); NULL = engine-owned stream.

@@ -133,18 +133,22 @@ def test_extreme_short_ratings_every_path(cfk, oracle_mod, monkeypatch, k, presp
 @pytest.mark.parametrize("scale", [1e-20, 1e-6, 1.0, 3e4, 1e12])
 def test_presplit_scale_extreme_factor_magnitudes(cfk, oracle_mod, scale):
     """The fp16 pre-split scales each opposite table by 2^s from its largest |x| (als_absmax, split_exp): tables of
-    any magnitude whose Gram fits fp32 -- far below the fp16 range, far beyond its 65504 maximum -- stay within the fp32 envelope, both halves,
-    k = 64 and 128."""
+    any magnitude whose Gram fits fp32 -- far below the fp16 range, far beyond its 65504 maximum -- stay within the
+    fp32 envelope, both halves, k = 64 and 128. Above scale 1, lambda grows with scale^2 so the systems keep their
+    conditioning (with lambda fixed, a 3e4-scaled table makes every short row's system singular in fp32 -- the
+    reference's own fp32 solve returns NaN there); below, lambda n I dominates anyway."""
     ds, b = _split_row_data(cfk, oracle_mod, seed=7)
+    lam = float(np.float32(LAM * max(1.0, scale) ** 2))
     for k in (64, 128):
         rng = np.random.default_rng(k)
         for side, rows, opp in ((0, b.movie, b.user), (1, b.user, b.movie)):
             F = rng.standard_normal((len(opp.ids), k)) * scale
-            ref = oracle_mod.update_side(rows, F, LAM, "f64")
-            ref32 = oracle_mod.update_side(rows, F.astype(np.float32), LAM, "f32")
+            ref = oracle_mod.update_side(rows, F, lam, "f64")
+            ref32 = oracle_mod.update_side(rows, F.astype(np.float32), lam, "f32")
+            assert np.all(np.isfinite(ref32))
             eng = _engine(cfk, k, "f32", side, ds.shard_block(side), len(opp.ids), F.astype(np.float32))
             assert eng.block_path(side)["presplit"]
-            eng.solve_half(side, LAM)
+            eng.solve_half(side, lam)
             got = eng.read_factors(side)
             eng.close()
             assert np.all(np.isfinite(got))

@@ -82,9 +82,10 @@ def _synthetic(cfk, oracle_mod, n_users=3000, n_movies=400, nnz=90_000, seed=11)
     return ds, oracle_mod.build_blocks(m, u, r)
 
 
-@pytest.mark.parametrize("k", [1, 5, 10, 16, 17, 31, 32, 33, 48, 63, 64, 65, 96, 127, 128])
+@pytest.mark.parametrize("k", [1, 5, 10, 16, 17, 31, 32, 33, 48, 63, 64, 65, 96, 127, 128, 129, 160, 256])
 def test_one_half_every_k_vs_oracle(cfk, oracle_mod, k):
-    """Both sides. f64 (VALU path) to 1e-7 max-rel. f32 (VALU k<32 / MFMA tile solve k>=32) against the exact
+    """Both sides. f64 (VALU path k <= 64, generic workgroup path above) to 1e-7 max-rel. f32 (VALU k<32 / MFMA tile
+    solve 32 <= k <= 128 / generic workgroup Cholesky k > 128, ALSAppRunner.java:18 takes any k) against the exact
     solution, held to the error envelope of the reference's OWN fp32 arithmetic on the same rows (the oracle's
     f32 mode restates EJML's fp32 LU): per-row norm-relative error p99 <= 2x and max <= 3x the reference's,
     with floors 2e-5 / 1e-4. The worst rows on both paths are users with one rating (A = y y^T + 0.05 I,
@@ -95,13 +96,16 @@ def test_one_half_every_k_vs_oracle(cfk, oracle_mod, k):
         blk = ds.shard_block(side)
         F = rng.random((len(opp.ids), k))
         ref = oracle_mod.update_side(rows, F, LAM, "f64")
-        if k <= 64:
-            got64 = _one_half(cfk, side, blk, F, k, "f64", len(opp.ids))
-            assert max_rel(got64, ref) <= 1e-7, (side, k)          # 10x inside the 1e-6 bar
-        else:                                                      # f64 parity mode covers k <= 64
-            from cfk_amd._lib import ALSError
-            with pytest.raises(ALSError, match="ALS_ERR_UNSUPPORTED"):
-                cfk.ALSEngine(k, "f64")
+        got64 = _one_half(cfk, side, blk, F, k, "f64", len(opp.ids))   # k > 64: the generic workgroup path
+        rel64 = np.linalg.norm(got64 - ref, axis=1) / np.linalg.norm(ref, axis=1)
+        if k <= 128:
+            # 10x inside the 1e-6 north-star bar on the VALU path (k <= 64), the bar itself on the generic path
+            assert max_rel(got64, ref) <= (1e-7 if k <= 64 else 1e-6), (side, k)
+        else:
+            # beyond 128 the per-element quotient (floor 1e-12 ||row||) of two fp64 solutions that both carry
+            # ~cond * eps of the row norm reaches 1.7e-6 (k = 129) / 2.8e-6 (k = 256) on near-zero elements of the
+            # users' rows (30 ratings, cond ~1e3); held to the row-norm error instead
+            assert max_rel(got64, ref) <= 1e-5 and rel64.max() <= 1e-10, (side, k, rel64.max())
         got32 = _one_half(cfk, side, blk, F.astype(np.float32), k, "f32", len(opp.ids))
         ref32 = oracle_mod.update_side(rows, F.astype(np.float32), LAM, "f32")
         norm = np.linalg.norm(ref, axis=1)

@@ -198,9 +198,9 @@ def test_error_behaviour(cfk, tmp_path):
     with pytest.raises(ALSError):
         cfk.ALSEngine(0, "f32")
     with pytest.raises(ALSError, match="ALS_ERR_UNSUPPORTED"):
-        cfk.ALSEngine(129, "f32")          # f32: 1..128
+        cfk.ALSEngine(1025, "f32")         # 1..1024 (beyond 128 fp32 / 64 fp64: the generic path)
     with pytest.raises(ALSError, match="ALS_ERR_UNSUPPORTED"):
-        cfk.ALSEngine(100, "f64")          # f64 parity mode: 1..64
+        cfk.ALSEngine(2000, "f64")
 
 
 def test_cli_arguments_missing_message():

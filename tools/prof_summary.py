@@ -139,6 +139,7 @@ def main(tag, name):
             cyc = sq["GRBM_GUI_ACTIVE"] / XCDS                   # GPU cycles of the launch (summed over XCDs)
             d["mfma_busy_frac"] = sq["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * SIMDS)
             d["valu_issue_frac"] = sq["SQ_INSTS_VALU"] / (cyc * SIMDS)
+            d["mfma_mops"] = {x: sq[x] for x in ("SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_INSTS_VALU_MFMA_MOPS_F16") if x in sq}
             d["wait_inst_any_frac"] = sq["SQ_WAIT_INST_ANY"] / sq["SQ_WAVE_CYCLES"]
             if tr_ms:
                 d["clock_ghz"] = cyc / (tr_ms * 1e-3) / 1e9
