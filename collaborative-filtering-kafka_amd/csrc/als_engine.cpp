@@ -50,7 +50,6 @@ struct Block {
     Task* d_tasks = nullptr;        // FULL + PARTIAL, sorted by work (longest first)
     Task* d_reduce = nullptr;       // REDUCE
     int32_t n_tasks = 0, n_reduce = 0, n_slots = 0;
-    int min_waves = 2;              // MFMA variant occupancy target chosen from the work plan
     double* d_task_se = nullptr;    // per-task squared-error partials
     std::vector<Task> h_tasks, h_reduce;   // host copies of the work plan (chunking re-sorts them)
     Task* d_ctasks = nullptr;       // chunk-major FULL + PARTIAL tasks (LPT inside each chunk)
@@ -502,9 +501,6 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
         // row (< 2^24) and the offset (< 2^32) must fit, also when ALS_PRESPLIT=1 forces the path
         if (n_opp_rows + 1 >= (1 << 24) || sb > (int64_t)UINT32_MAX) ps = false;
         blk.presplit = ps;
-        // waves per SIMD of the main launch: the pre-split Gram runs 3 at KP = 64 (an 8-KB LDS image per wave; the
-        // other waves hide its latency), the other KP = 32/64 MFMA variants 2 (KP = 128: 1, fixed by the launch)
-        blk.min_waves = ps ? 3 : 2;
         if (ps && (size_t)sb > e->split_bytes) {
             (void)hipFree(e->d_split);
             e->d_split = nullptr;
@@ -837,7 +833,7 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
         a.col_ps = b.d_col_ps;
         a.amax = e->d_amax;
     }
-    HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves, b.presplit, false));
+    HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.presplit, false));
     if (side_dual) HIP_TRY(hipStreamWaitEvent(e->side_stream, e->fork, 0));
     for (int c = 0; c < 3; ++c)
         if (dl.n[c] > 0) {
@@ -855,7 +851,7 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
         a.tasks = reduce;
         a.n_tasks = n_reduce;
         a.gen += e->debug_gen_skew;
-        HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.min_waves, false, true));
+        HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, false, true));
     }
     if (e->timing) {
         HIP_TRY(hipEventRecord(rec.ev[2], e->stream));

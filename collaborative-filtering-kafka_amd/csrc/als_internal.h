@@ -117,10 +117,11 @@ GenericPlan generic_plan(int precision, int kp);
 hipError_t launch_generic(int precision, int kp, const SolveArgs& a, hipStream_t s);
 
 // Launch helpers (defined in als_kernels.hip). Return hipSuccess or the launch error.
-// min_waves: occupancy target (waves per SIMD) of the MFMA variant (__launch_bounds__ second argument).
-// reduce: `a.tasks` are REDUCE tasks (launched after the FULL/PARTIAL launch of the same half).
-hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, int min_waves,
-                        bool presplit, bool reduce);
+// The variant (and its occupancy) follows from (precision, kp, path, presplit). presplit: the Gram reads the pre-split
+// opposite table (a.opp_split). reduce: `a.tasks` are REDUCE tasks (launched after the FULL/PARTIAL launch of the
+// same half).
+hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, bool presplit,
+                        bool reduce);
 // Short rows in entry space (als_solve_dual): fp32 split path, kp 64 with cd 2, kp 128 with cd 2 or 4 (rows of
 // 16 * cd padded entries, i.e. cd / 2 blocks); `a.tasks` are FULL tasks of such rows.
 hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s);

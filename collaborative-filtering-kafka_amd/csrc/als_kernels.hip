@@ -611,6 +611,10 @@ __host__ __device__ constexpr int la_item_I(int C, int P, int t) {   // -1: the 
     }
     return -2;
 }
+// waves per SIMD of the pre-split KP = 64 kernel (register budget 512 / waves; LDS 16 x 8.25 KB at 4)
+#ifndef CFK_PS64_WAVES
+#define CFK_PS64_WAVES 4
+#endif
 #ifndef CFK_SOLVE_LOOKAHEAD
 #define CFK_SOLVE_LOOKAHEAD 1
 #endif
@@ -678,7 +682,16 @@ __device__ __forceinline__ int logical_entry(int q) {
     return q - w + (w % BLOCK_SUBSTEPS) * 4 + w / BLOCK_SUBSTEPS;
 }
 
-// T: working tiles (RegTiles / LdsTiles), A0: kept copy of the scaled system (RegStore / LdsTiles).
+// Tag for solve_tiles' A0: keep NO copy of the system; a refinement step (rare: every Netflix-shape user row passes
+// the pivot gate, tools/refine_accuracy.py) forms its residual from the factor rows instead, r = b - D (G (D x) +
+// lambda n D x) with G z = sum_e y_e (y_e . z) over the row's entries -- the exact fp32 rows, so the step also
+// corrects the pre-split Gram's 2^-22 representation. Frees the copy's registers (4 waves per SIMD on the pre-split
+// KP = 64 path instead of 3).
+struct RowResidual {
+    __device__ __forceinline__ void put(int, const f32x4&) {}
+};
+
+// T: working tiles (RegTiles / LdsTiles), A0: kept copy of the scaled system (RegStore / LdsTiles), or RowResidual.
 // DUAL: the system is the entry Gram of a short row (als_solve_dual): unknown 16b + j = the row's entry at
 // physical position 16b + j, real when that entry exists (padding entries get an identity row), and the
 // solution alpha goes to buf[16b + j] (read by the caller after a wave_sync) instead of a factor row.
@@ -721,7 +734,6 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
     const int jr = j & 3;
     const bool diag_lane = opaque(j >> 2) == g;   // lane holds a diagonal entry, in register j & 3
     float scol[C];
-    f32x4 srow[C];
 #pragma unroll
     for (int b = 0; b < C; ++b) {
         f32x4 t = T.get(tile_index<C>(b, b));
@@ -739,21 +751,20 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
     }
     wave_sync();
 #pragma unroll
-    for (int b = 0; b < C; ++b) {
-        scol[b] = buf[16 * b + j];
-        srow[b] = *(const f32x4*)(buf + 16 * b + 4 * g);
-    }
-    wave_sync();
+    for (int b = 0; b < C; ++b) scol[b] = buf[16 * b + j];
 #pragma unroll
-    for (int I = 0; I < C; ++I)
+    for (int I = 0; I < C; ++I) {
+        const f32x4 srow = *(const f32x4*)(buf + 16 * I + 4 * g);   // s for rows 4g .. 4g + 3 of block I
 #pragma unroll
         for (int J = I; J < C; ++J) {
             f32x4 t = T.get(tile_index<C>(I, J));
 #pragma unroll
-            for (int r = 0; r < 4; ++r) t[r] *= srow[I][r] * scol[J];
+            for (int r = 0; r < 4; ++r) t[r] *= srow[r] * scol[J];
             T.put(tile_index<C>(I, J), t);
             A0.put(tile_index<C>(I, J), t);
         }
+    }
+    wave_sync();
     float b0[C];
 #pragma unroll
     for (int b = 0; b < C; ++b) b0[b] = col_sum(rhs_acc[b]) * scol[b];
@@ -903,7 +914,44 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
         return;
     }
 
-    // ---- one refinement step: r = b - A x over the kept upper tiles (A_IJ and A_IJ^T), x += A^{-1} r ----
+    // ---- one refinement step: r = b - A x, x += A^{-1} r ----
+    float r[C];
+    if constexpr (std::is_same<KT, RowResidual>::value) {
+        static_assert(!DUAL, "row residual: primal systems only");
+        // z = D x (lane (g, j), block b: feature C j + b, the layout of a C-float piece of a factor row)
+        float z[C], acc[C];
+#pragma unroll
+        for (int b = 0; b < C; ++b) {
+            z[b] = x[b] * scol[b];
+            acc[b] = 0.f;
+        }
+        using VT = typename VecC<C>::type;
+        typedef int i32x4 __attribute__((ext_vector_type(4)));
+        const char* obase = (const char*)a.opp + (uint32_t)(C * j * sizeof(float));
+        const int32_t* cb = a.col + tk.begin + 8 * g;   // group g: physical entries 8 g .. 8 g + 7 of each block
+        const int nblk = (tk.nsteps + BLOCK_SUBSTEPS - 1) / BLOCK_SUBSTEPS;
+        for (int blk = 0; blk < nblk; ++blk) {
+            const i32x4 c0 = *(const i32x4*)(cb + blk * BLOCK_ENTRIES);
+            const i32x4 c1 = *(const i32x4*)(cb + blk * BLOCK_ENTRIES + 4);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {   // padding entries read the zero sentinel row
+                const uint32_t row = (uint32_t)(t < 4 ? c0[t] : c1[t - 4]);
+                const VT y = *(const VT*)(obase + row * (uint32_t)(16 * C * sizeof(float)));
+                float p = 0.f;
+#pragma unroll
+                for (int b = 0; b < C; ++b) p += y[b] * z[b];
+                p = row_lane_bcast<15>(row_sum_to_last(p));   // y_e . z over the 16 lanes of the row group
+#pragma unroll
+                for (int b = 0; b < C; ++b) acc[b] += y[b] * p;
+            }
+        }
+        const float reg = a.lambda * (float)tk.ndeg;
+#pragma unroll
+        for (int b = 0; b < C; ++b) {
+            const float gz = col_sum(acc[b]);
+            r[b] = b0[b] - (is_real(b) ? scol[b] * (gz + reg * z[b]) : x[b]);   // padded features: identity rows
+        }
+    } else {
     wave_sync();
     if (g == 0) {
 #pragma unroll
@@ -944,9 +992,9 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
         for (int b = 0; b < C; ++b) *(f32x4*)(buf + 16 * b + 4 * g) = w[b];
     }
     wave_sync();
-    float r[C];
 #pragma unroll
     for (int b = 0; b < C; ++b) r[b] = b0[b] - buf[16 * b + j] - (C > 1 ? col_sum(res[b]) : 0.f);
+    }
     float dx[C];
     solve_vec(r, dx);
     float xs[C];
@@ -1205,20 +1253,22 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                     });
                 });
             };
+            auto read1 = [&](auto PL_, auto B_) {
+                constexpr int pl = decltype(PL_)::value, b = decltype(B_)::value;
+                u32x4 P;
+                static_for<0, 2>([&](auto H_) {
+                    constexpr int h = decltype(H_)::value;
+                    const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (lds_s16x4*)(img + rd[b & 3] + ((pl * NH + (b >> 2)) * 4 + h) * 1024));
+                    const u32x2 w = __builtin_bit_cast(u32x2, v);
+                    P[2 * h] = w[0];
+                    P[2 * h + 1] = w[1];
+                });
+                return P;
+            };
             auto read = [&](u32x4 (&P)[NPL][C]) {
                 static_for<0, NPL>([&](auto PL_) {
-                    constexpr int pl = decltype(PL_)::value;
-                    static_for<0, C>([&](auto B_) {
-                        constexpr int b = decltype(B_)::value;
-                        static_for<0, 2>([&](auto H_) {
-                            constexpr int h = decltype(H_)::value;
-                            const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                                (lds_s16x4*)(img + rd[b & 3] + ((pl * NH + (b >> 2)) * 4 + h) * 1024));
-                            const u32x2 w = __builtin_bit_cast(u32x2, v);
-                            P[pl][b][2 * h] = w[0];
-                            P[pl][b][2 * h + 1] = w[1];
-                        });
-                    });
+                    static_for<0, C>([&](auto B_) { P[decltype(PL_)::value][decltype(B_)::value] = read1(PL_, B_); });
                 });
             };
             if (nblk > 0) {
@@ -1232,11 +1282,11 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                 cv = cp[8 * min(1, lastb)];
                 for (int b = 0; b < nblk; ++b) {
                     const u32x4 R = Rn;
-                    u32x4 P[NPL][C];
                     // every vector-memory op of this wave done: this block's LDS-DMA (and the column / rating loads
                     // the DMA issue and the MFMAs below need anyway) -- explicit, not left to the compiler's tracking
                     // of LDS-DMA writes (tests/test_isa_guard.py checks it)
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    u32x4 P[NPL][C];
                     read(P);
                     // the operands are in registers before the image is overwritten by the next block's DMA
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1252,11 +1302,11 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
 #pragma unroll
             for (int t = 0; t < Acc::NT; ++t)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc.g[t][r] = ldexpf(ldexpf(acc.g[t][r], -sc), -sc);
+                for (int r = 0; r < 4; ++r) acc.g[t][r] = ldexpf(acc.g[t][r], -2 * sc);
 #pragma unroll
             for (int b = 0; b < C; ++b)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) E[b][r] = ldexpf(ldexpf(E[b][r], -sc), -sc);
+                for (int r = 0; r < 4; ++r) E[b][r] = ldexpf(E[b][r], -2 * sc);
             // RHS tiles (row i of block b = feature C i + b; column 0 = Y^T rh, column 8 = Y^T rm) -> the per-lane
             // partial layout of the other paths: lane (0, j) holds feature C j + b, the other rows zero (col_sum
             // restores it)
@@ -1631,6 +1681,10 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
         RegStore<C> A0;
 #pragma unroll
         for (int p = 0; p < Acc::NT; ++p) T.put(p, acc.g[p]);
+        solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
+    } else if constexpr (PRESPLIT && !REDUCE) {
+        RegTiles<C> T{acc.g};
+        RowResidual A0;
         solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
     } else {
         RegTiles<C> T{acc.g};
@@ -2232,19 +2286,19 @@ hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, int min_waves,
-                        bool presplit, bool reduce) {
+hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, bool presplit,
+                        bool reduce) {
     if (path == Path::GENERIC) return reduce ? hipErrorInvalidValue : launch_generic(precision, kp, a, s);
     if (precision == 0) {
-        // occupancy (waves per SIMD) per variant: KP <= 64 two, the pre-split KP = 64 Gram three, KP = 128 one
-        (void)min_waves;
+        // occupancy (waves per SIMD) per variant: KP <= 64 two, the pre-split KP = 64 Gram four (CFK_PS64_WAVES),
+        // KP = 128 one
         if (path == Path::MFMA) {
             if (kp == 32) return launch_solve_t<float, 32, Path::MFMA, 2>(a, s, reduce);
             if (kp == 64) return launch_solve_t<float, 64, Path::MFMA, 2>(a, s, reduce);
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA, 1>(a, s, reduce);
         } else if (path == Path::MFMA_SPLIT) {
             if (kp == 32) return launch_solve_t<float, 32, Path::MFMA_SPLIT, 2>(a, s, reduce);
-            if (kp == 64 && presplit) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 3, true>(a, s, reduce);
+            if (kp == 64 && presplit) return launch_solve_t<float, 64, Path::MFMA_SPLIT, CFK_PS64_WAVES, true>(a, s, reduce);
             if (kp == 64) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2>(a, s, reduce);
             if (kp == 128 && presplit) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1, true>(a, s, reduce);
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1>(a, s, reduce);

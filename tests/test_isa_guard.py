@@ -22,7 +22,8 @@ import pytest
 from conftest import ROOT
 
 LLVM = "/opt/rocm/lib/llvm/bin"
-LIB = os.path.join(ROOT, "collaborative-filtering-kafka_amd", "build", "libcfk_als.so")
+# CFK_ISA_LIB: check another build of the library (an A/B variant) instead of the product
+LIB = os.environ.get("CFK_ISA_LIB") or os.path.join(ROOT, "collaborative-filtering-kafka_amd", "build", "libcfk_als.so")
 REG = re.compile(r"([va])\[(\d+):(\d+)\]|([va])(\d+)\b")
 
 
