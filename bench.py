@@ -313,7 +313,7 @@ def main():
             # ratings (fp16 rh / rm pairs on the pre-split path) and the written factor rows
             dual_entries = sum(32 * (c_ + 1) * n for c_, n in enumerate(dual))
             main_entries = main_blocks * 32
-            gathered = (main_entries * (4 * kp + 4 + (4 if path["presplit"] else 4)) + dual_entries * (4 * kp + 8)
+            gathered = (main_entries * (4 * kp + 8) + dual_entries * (4 * kp + 8)
                         + 4 * kp * i["n_rows"])
             opp_rows = info["user" if side == "movie" else "movie"]["n_slots"] + 1
             table_bytes = opp_rows * 4 * kp
@@ -326,7 +326,8 @@ def main():
             g_bytes = fab if (fab and gceil == IC_GATHER_CEILING_GBS) else gathered
             gather_frac = g_bytes / t_s / 1e9 / gceil
             d = {
-                "kernel": f"als_solve_mfma<{kp},{1 if kp == 128 else (3 if path['presplit'] else 2)},split,"
+                # <KP, waves per SIMD, ...>: the instantiations launch_solve picks (als_kernels.hip, CFK_PS64_WAVES)
+                "kernel": f"als_solve_mfma<{kp},{1 if kp == 128 else (4 if path['presplit'] else 2)},split,"
                           f"{'presplit f16' if path['presplit'] else 'on-the-fly bf16 split'}> + als_solve_dual "
                           f"(short rows)",
                 "avg_launch_ms": g_ms[side], "reduce_launch_ms": r_ms[side],
