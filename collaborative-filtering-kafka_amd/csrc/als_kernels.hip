@@ -615,6 +615,12 @@ __host__ __device__ constexpr int la_item_I(int C, int P, int t) {   // -1: the 
 #ifndef CFK_PS64_WAVES
 #define CFK_PS64_WAVES 4
 #endif
+#ifndef CFK_OTF_ROWRES
+#define CFK_OTF_ROWRES 0
+#endif
+#ifndef CFK_OTF64_WAVES
+#define CFK_OTF64_WAVES 2
+#endif
 #ifndef CFK_SOLVE_LOOKAHEAD
 #define CFK_SOLVE_LOOKAHEAD 1
 #endif
@@ -631,10 +637,10 @@ __host__ __device__ constexpr int la_item_I(int C, int P, int t) {   // -1: the 
 // (scaled, regularised) Gram kept in registers: r = b - A x, x += solve(r). That brings the fp32 error
 // below the reference's own fp32 LU (tests/test_gpu_parity.py). Vectors are held "lane (g, j) = element j"
 // of each block; buf is KP floats of per-wave LDS.
-// Tile storage of the solve. Up to KP = 64 the tiles stay in the MFMA accumulator registers (RegTiles);
-// at KP = 128 (36 tiles = 144 registers per copy; the solve's VALU work needs them in the 256 architected
-// VGPRs) the working tiles live in per-wave LDS ([tile][lane][reg], CFK_LDS_B128; or [tile][reg][lane]: conflict-free b32
-// accesses) and are loaded a tile at a time (LdsTiles).
+// Tile storage of the solve. Up to KP = 64 the tiles stay in the MFMA accumulator registers (RegTiles), and so do
+// they at KP = 128 on the pre-split path, which keeps no copy of the system (RowResidual); the other KP = 128 paths
+// (36 tiles = 144 registers per copy, plus the kept copy) hold the working tiles in per-wave LDS ([tile][lane][reg],
+// CFK_LDS_B128; or [tile][reg][lane]: conflict-free b32 accesses), loaded a tile at a time (LdsTiles).
 template <int C>
 struct RegTiles {
     f32x4* t;
@@ -1067,10 +1073,14 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
     using Acc = MfmaAcc<C>;
     using VT = typename VecC<C>::type;
     __shared__ __attribute__((aligned(16))) float sbuf[NW][KP];
-    constexpr int TL = tile_lds_floats<C>();
+    // KP = 128 keeps the solve's working tiles in per-wave LDS, except on the pre-split path: its solve keeps no copy
+    // of the system (RowResidual), which leaves the registers for the tiles themselves (user half 11.4 -> 10.5 ms)
+    constexpr bool TILES_LDS = tiles_in_lds<C>() && !(PRESPLIT && !REDUCE);
+    constexpr int TL = TILES_LDS ? tile_lds_floats<C>() : 0;
     __shared__ __attribute__((aligned(16))) float tiles_lds[NW][TL > 0 ? TL : 1];
+    (void)tiles_lds;
     // pre-split Gram: one block's LDS image per wave (LDS-DMA target)
-    constexpr int STAGE = (PRESPLIT && !REDUCE && !tiles_in_lds<C>()) ? 2 * C * 1024 : 16;
+    constexpr int STAGE = (PRESPLIT && !REDUCE) ? 2 * C * 1024 : 16;
     __shared__ __attribute__((aligned(1024))) unsigned char stage_lds[NW][STAGE];
     (void)stage_lds;
 
@@ -1209,21 +1219,14 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             // (pl, b) of lane (g, 4 q + p) = two ds_read_b64_tr_b16 (h = 0, 1: entries 8 g + 4 h + 0..3), lane
             // 4 q + p addressing entry 8 g + 4 h + q, plane positions 16 b + 4 p .. + 3 (features C j + b,
             // j = 4 p .. 4 p + 3); the 16 lanes of a group receive features j = 0..15 of their 4 entries: exactly
-            // the MFMA A/B operand, no lane movement. KP = 128 keeps the image in the wave's solve-tile area
-            // (tiles_lds, 36 KB): the tiles are written only after the last block's reads.
+            // the MFMA A/B operand, no lane movement.
             typedef short s16x4 __attribute__((ext_vector_type(4)));
             typedef __attribute__((address_space(3))) void lds_void;
             typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
             constexpr int NH = C / 4;              // 128-B halves per plane
             constexpr int IMG = NPL * C * 1024;
-            unsigned char* img;
-            if constexpr (tiles_in_lds<C>()) {
-                static_assert(sizeof(tiles_lds[0]) >= IMG, "stage image in the tile area");
-                img = (unsigned char*)tiles_lds[uni(wave)];
-            } else {
-                static_assert(sizeof(stage_lds[0]) >= IMG, "stage image");
-                img = stage_lds[uni(wave)];
-            }
+            static_assert(sizeof(stage_lds[0]) >= IMG, "stage image");
+            unsigned char* img = stage_lds[uni(wave)];
             const int r8 = lane >> 3;
             const uint32_t ld_off = 16u * (uint32_t)((lane & 7) ^ (2 * (r8 >> 1)));
             const int q = (lane >> 2) & 3, p = lane & 3, rr = 4 * (g & 1) + q;
@@ -1676,13 +1679,13 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
         }
         return;
     }
-    if constexpr (tiles_in_lds<C>()) {
+    if constexpr (TILES_LDS) {
         LdsTiles T{tiles_lds[wave] + (CFK_LDS_B128 ? 4 : 1) * lane};
         RegStore<C> A0;
 #pragma unroll
         for (int p = 0; p < Acc::NT; ++p) T.put(p, acc.g[p]);
         solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
-    } else if constexpr (PRESPLIT && !REDUCE) {
+    } else if constexpr ((PRESPLIT || (SPLIT && CFK_OTF_ROWRES)) && !REDUCE) {
         RegTiles<C> T{acc.g};
         RowResidual A0;
         solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
@@ -2299,7 +2302,7 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
         } else if (path == Path::MFMA_SPLIT) {
             if (kp == 32) return launch_solve_t<float, 32, Path::MFMA_SPLIT, 2>(a, s, reduce);
             if (kp == 64 && presplit) return launch_solve_t<float, 64, Path::MFMA_SPLIT, CFK_PS64_WAVES, true>(a, s, reduce);
-            if (kp == 64) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2>(a, s, reduce);
+            if (kp == 64) return launch_solve_t<float, 64, Path::MFMA_SPLIT, CFK_OTF64_WAVES>(a, s, reduce);
             if (kp == 128 && presplit) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1, true>(a, s, reduce);
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1>(a, s, reduce);
         } else {

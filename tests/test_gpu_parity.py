@@ -575,7 +575,8 @@ def test_gram_variants_vs_oracle(cfk, oracle_mod, monkeypatch):
     ALS_GRAM=f32 (exact v_mfma_f32_16x16x4_f32 Gram instead of the split-bf16 one), ALS_PRESPLIT=0 (the k = 64
     user half on the on-the-fly split instead of the pre-split LDS-DMA Gram; ALS_PRESPLIT=1 is the default there),
     ALS_REFINE_MIN_PIVOT=2 (the refinement step on every row; the product library clamps lower values to the
-    validated 0.45 gate, so =0 is the default path), and ALS_DUAL_SIDE=0 (entry-space launches on the engine stream
+    validated 0.45 gate, so =0 is the default path; with ALS_PRESPLIT=0 as well: the matrix-free refinement of the
+    on-the-fly path), and ALS_DUAL_SIDE=0 (entry-space launches on the engine stream
     instead of the side stream, bitwise equal to the default)."""
     ds, b = _synthetic(cfk, oracle_mod)
     blk = ds.shard_block(1)
@@ -586,7 +587,8 @@ def test_gram_variants_vs_oracle(cfk, oracle_mod, monkeypatch):
         ref32 = oracle_mod.update_side(b.user, F.astype(np.float32), LAM, "f32")
         outs = {}
         for env in ({}, {"ALS_GRAM": "f32"}, {"ALS_DUAL_SIDE": "0"}, {"ALS_PRESPLIT": "0"},
-                    {"ALS_REFINE_MIN_PIVOT": "2"}, {"ALS_REFINE_MIN_PIVOT": "0"}):
+                    {"ALS_REFINE_MIN_PIVOT": "2"}, {"ALS_REFINE_MIN_PIVOT": "0"},
+                    {"ALS_PRESPLIT": "0", "ALS_REFINE_MIN_PIVOT": "2"}):
             for name in knobs:
                 monkeypatch.delenv(name, raising=False)
             for name, v in env.items():
