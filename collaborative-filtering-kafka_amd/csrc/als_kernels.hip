@@ -615,12 +615,6 @@ __host__ __device__ constexpr int la_item_I(int C, int P, int t) {   // -1: the 
 #ifndef CFK_PS64_WAVES
 #define CFK_PS64_WAVES 4
 #endif
-#ifndef CFK_OTF_ROWRES
-#define CFK_OTF_ROWRES 0
-#endif
-#ifndef CFK_OTF64_WAVES
-#define CFK_OTF64_WAVES 2
-#endif
 #ifndef CFK_SOLVE_LOOKAHEAD
 #define CFK_SOLVE_LOOKAHEAD 1
 #endif
@@ -1685,7 +1679,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
 #pragma unroll
         for (int p = 0; p < Acc::NT; ++p) T.put(p, acc.g[p]);
         solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
-    } else if constexpr ((PRESPLIT || (SPLIT && CFK_OTF_ROWRES)) && !REDUCE) {
+    } else if constexpr (PRESPLIT && !REDUCE) {
         RegTiles<C> T{acc.g};
         RowResidual A0;
         solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
@@ -2302,7 +2296,7 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
         } else if (path == Path::MFMA_SPLIT) {
             if (kp == 32) return launch_solve_t<float, 32, Path::MFMA_SPLIT, 2>(a, s, reduce);
             if (kp == 64 && presplit) return launch_solve_t<float, 64, Path::MFMA_SPLIT, CFK_PS64_WAVES, true>(a, s, reduce);
-            if (kp == 64) return launch_solve_t<float, 64, Path::MFMA_SPLIT, CFK_OTF64_WAVES>(a, s, reduce);
+            if (kp == 64) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2>(a, s, reduce);
             if (kp == 128 && presplit) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1, true>(a, s, reduce);
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1>(a, s, reduce);
         } else {
