@@ -149,7 +149,9 @@ def main(tag, name):
                                   "mfma_busy_frac": gr["SQ_VALU_MFMA_BUSY_CYCLES"] / (gcyc * SIMDS),
                                   "valu_issue_frac": gr["SQ_INSTS_VALU"] / (gcyc * SIMDS)}
                 scyc = cyc - gcyc
-                if scyc > 0:
+                # the difference of two launches: meaningful only when the solve is a real share of the cycles (on the
+                # gather-bound movie launch it is within the run-to-run noise of the Gram)
+                if scyc > 0.05 * cyc:
                     d["solve_phase"] = {
                         "cycles_frac": scyc / cyc,
                         "mfma_busy_frac": (sq["SQ_VALU_MFMA_BUSY_CYCLES"] - gr["SQ_VALU_MFMA_BUSY_CYCLES"]) / (scyc * SIMDS),
