@@ -1008,8 +1008,9 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 template <int KP>
 constexpr int mfma_waves() { return WAVES; }
 
-// Largest |x| of a table (the pre-split scale, split_exp): grid-stride over 16-B vectors, wave max, one vector-memory
-// atomicMax per wave on the bits (non-negative floats order as unsigned integers). *out is zeroed before the launch.
+// Largest |x| of a table (the pre-split scale, split_exp): grid-stride over 16-B vectors, workgroup max, one
+// vector-memory atomicMax per workgroup on the bits (non-negative floats order as unsigned integers). *out is zeroed
+// before the launch.
 __global__ __launch_bounds__(256) void als_absmax(const u32x4* __restrict__ src, int64_t n4, uint32_t* __restrict__ out) {
     uint32_t m = 0;
     const int64_t stride = (int64_t)gridDim.x * 256;
@@ -1019,7 +1020,14 @@ __global__ __launch_bounds__(256) void als_absmax(const u32x4* __restrict__ src,
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
-    if ((threadIdx.x & 63) == 0 && m != 0) atomicMax(out, m);
+    // one atomic per workgroup: thousands of same-address atomics serialise (53 us for the 4.5 MB M table)
+    __shared__ uint32_t wm[4];
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
+        if (m != 0) atomicMax(out, m);
+    }
 }
 
 // fp32 table -> fp16 h/m planes (presplit_row_bytes(KP) per row, als_internal.h) at the table's scale 2^s: thread
@@ -2252,7 +2260,8 @@ hipError_t launch_absmax(const float* src, int64_t n_floats, uint32_t* amax, hip
     if (e != hipSuccess || n_floats <= 0) return e;
     if (n_floats % 4) return hipErrorInvalidValue;   // whole KP-wide rows
     const int64_t n4 = n_floats / 4;
-    const int64_t blocks = std::min<int64_t>((n4 + 255) / 256, 2048);
+    // >= 8 vectors per thread, at most 512 workgroups (= atomics)
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n4 + 2047) / 2048, 512));
     als_absmax<<<(unsigned)blocks, 256, 0, s>>>((const u32x4*)src, n4, amax);
     return hipGetLastError();
 }
