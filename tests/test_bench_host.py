@@ -1,0 +1,62 @@
+"""bench.py's host-side contract pieces that need no GPU: counters are used only for the library they were profiled
+with, the CPU-baseline legs never exceed the process's CPU share (item 7), and the diagnostics
+build is refused before anything is measured."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def _write_counters(tmp_path, monkeypatch, **fields):
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    c = {"k": 64, "nnz": 1000, "lib_sha256": "a" * 64, "source": "profiles/rXX", "per_side": {}}
+    c.update(fields)
+    (prof / "counters_k64.json").write_text(json.dumps(c))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+
+
+def test_counters_used_for_the_profiled_library_only(tmp_path, monkeypatch):
+    _write_counters(tmp_path, monkeypatch)
+    c, why = bench.load_counters(64, 1000, "a" * 64)
+    assert c is not None and why is None
+    c, why = bench.load_counters(64, 1000, "b" * 64)
+    assert c is None and why.startswith("stale:") and "aaaaaaaaaaaa" in why and "bbbbbbbbbbbb" in why
+
+
+def test_counters_of_another_workload_are_dropped(tmp_path, monkeypatch):
+    _write_counters(tmp_path, monkeypatch)
+    assert bench.load_counters(64, 2000, "a" * 64)[0] is None
+    (tmp_path / "profiles" / "counters_k64.json").unlink()
+    c, why = bench.load_counters(64, 1000, "a" * 64)
+    assert c is None and why.startswith("no ")
+
+
+def test_committed_counters_carry_a_library_hash():
+    for k in (64, 128):
+        c = json.load(open(os.path.join(ROOT, "profiles", f"counters_k{k}.json")))
+        assert c["k"] == k and len(c["lib_sha256"]) == 64, k
+        assert set(c["per_side"]) >= {"movie", "user"}, k
+
+
+def test_cpu_share_honours_affinity_and_omp(monkeypatch):
+    monkeypatch.delenv("OMP_NUM_THREADS", raising=False)
+    n, src = bench.cpu_share()
+    assert 1 <= n <= len(os.sched_getaffinity(0)) and src.startswith("affinity")
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    n3, src3 = bench.cpu_share()
+    assert n3 == min(3, n) and "OMP_NUM_THREADS 3" in src3
+
+
+def test_bench_refuses_the_debug_library():
+    env = dict(os.environ, CFK_ALS_LIB=os.path.join(ROOT, "collaborative-filtering-kafka_amd", "build_debug",
+                                                    "libcfk_als.so"))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "refused" in r.stderr
