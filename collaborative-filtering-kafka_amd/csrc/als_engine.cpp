@@ -108,6 +108,11 @@ struct als_engine {
     void* h_stage = nullptr;        // pinned staging of als_write_factors / als_read_factors (copy kernels)
     size_t stage_bytes = 0;
     uint32_t* d_integrity = nullptr;   // cfk::INTEGRITY_WORDS: partial slots that failed their check
+    int* d_queue = nullptr;         // task counter of the pipelined pre-split launch (cfk::launch_solve_pc)
+    int cu_count = 0;               // compute units of the device: the pipelined launch's grid
+    // pre-split halves through the pipelined launch (Gram waves hand systems to solver waves, cfk::launch_solve_pc)
+    // with ALS_PC=1; default: the one-kernel launch (each wave Gram then solve)
+    bool pipelined = false;
     uint32_t gen = 0;               // launch generation of the next PARTIAL/REDUCE pair
     int32_t debug_flags = 0;        // debug build only (CFK_DEBUG_KNOBS): ALS_DEBUG_SKIP_SOLVE / _REFINE
     uint32_t debug_gen_skew = 0;    // debug build only: ALS_DEBUG_REDUCE_GEN_SKEW=n, REDUCE decodes with generation
@@ -116,6 +121,8 @@ struct als_engine {
     // path where always refining puts it (0.41, tools/refine_accuracy.py; 0.30 lets it reach 1.2), and skips the
     // step for nearly every Netflix-shape row (k = 128 user half 17.7 -> 14.9 ms); > 1 always refines
     float refine_min_pivot = 0.45f;
+    int32_t debug_extra_lds = 0;    // debug build only: ALS_DEBUG_EXTRA_LDS=bytes of unused LDS per main-launch
+                                    // workgroup (occupancy sweeps of the MFMA kernels)
     bool debug_fixed_gen = false;   // debug build only: ALS_DEBUG_FIXED_GEN=1, every launch uses generation 1, so
                                     // partial slots of repeated launches are bitwise comparable (diagnostics)
     ncclComm_t comm = nullptr;      // RCCL communicator over the G engines (one per GPU) of a sharded run
@@ -161,6 +168,11 @@ int sync_checked(als_engine* e) {
     HIP_TRY(hipStreamSynchronize(e->stream));
     uint32_t rec[cfk::INTEGRITY_WORDS];
     HIP_TRY(hipMemcpy(rec, e->d_integrity, sizeof(rec), hipMemcpyDeviceToHost));
+    if (rec[0] != 0 && (int32_t)rec[2] == cfk::PC_TIMEOUT_SLOT)
+        return fail(ALS_ERR_INTEGRITY,
+                    "%u waves of a pipelined launch (generation %u) gave up waiting for a hand-off slot (first: row "
+                    "%d): its results are incomplete",
+                    rec[0], rec[1], (int32_t)rec[3]);
     if (rec[0] != 0)
         return fail(ALS_ERR_INTEGRITY,
                     "%u REDUCE tasks found partial slots that failed their check (first: launch generation %u, slot "
@@ -269,6 +281,7 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
     // weaken the partial-slot check, so they exist in the debug build only
     if (const char* env = getenv("ALS_DEBUG_REDUCE_GEN_SKEW")) e->debug_gen_skew = (uint32_t)atoi(env);
     if (const char* env = getenv("ALS_DEBUG_FIXED_GEN")) e->debug_fixed_gen = env[0] == '1';
+    if (const char* env = getenv("ALS_DEBUG_EXTRA_LDS")) e->debug_extra_lds = atoi(env);
 #endif
     if (const char* env = getenv("ALS_REFINE_MIN_PIVOT")) {
         // the product library can only refine MORE often than the validated gate (> 1: every row); thresholds
@@ -279,18 +292,22 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
 #endif
     }
     if (const char* env = getenv("ALS_DUAL_SIDE")) e->dual_side = env[0] != '0';
+    if (const char* env = getenv("ALS_PC")) e->pipelined = env[0] == '1';
     hipError_t st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (st != hipSuccess) {
         delete e;
         return fail(ALS_ERR_DEVICE, "hipStreamCreate: %s", hipGetErrorString(st));
     }
     e->own_stream = true;
-    st = hipMalloc((void**)&e->d_integrity, cfk::INTEGRITY_WORDS * sizeof(uint32_t));
+    st = hipDeviceGetAttribute(&e->cu_count, hipDeviceAttributeMultiprocessorCount, device);
+    if (st == hipSuccess) st = hipMalloc((void**)&e->d_queue, sizeof(int));
+    if (st == hipSuccess) st = hipMalloc((void**)&e->d_integrity, cfk::INTEGRITY_WORDS * sizeof(uint32_t));
     if (st == hipSuccess) st = hipMemset(e->d_integrity, 0, cfk::INTEGRITY_WORDS * sizeof(uint32_t));
     if (st == hipSuccess) st = hipMalloc((void**)&e->d_amax, sizeof(uint32_t));
     if (st != hipSuccess) {
         (void)hipStreamDestroy(e->stream);
         (void)hipFree(e->d_integrity);
+        (void)hipFree(e->d_queue);
         (void)hipFree(e->d_amax);
         delete e;
         return fail(ALS_ERR_DEVICE, "integrity record: %s", hipGetErrorString(st));
@@ -310,6 +327,7 @@ int als_engine_destroy(als_engine* e) {
     (void)hipFree(e->d_split);
     (void)hipHostFree(e->h_stage);
     (void)hipFree(e->d_integrity);
+    (void)hipFree(e->d_queue);
     (void)hipFree(e->d_amax);
     for (auto& rec : e->pending)
         for (auto ev : rec.ev) (void)hipEventDestroy(ev);
@@ -463,6 +481,18 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     }
     // Longest tasks first (LPT): the grid drains with a short tail.
     std::stable_sort(tasks.begin(), tasks.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
+    // ALS_TASK_ORDER=random (measurement knob): a seeded shuffle of the main launch's tasks instead of LPT
+    if (const char* env = getenv("ALS_TASK_ORDER")) {
+        if (std::strcmp(env, "random") == 0) {
+            uint64_t x = 0x9e3779b97f4a7c15ull;
+            for (size_t i = tasks.size(); i > 1; --i) {
+                x ^= x << 13;
+                x ^= x >> 7;
+                x ^= x << 17;
+                std::swap(tasks[i - 1], tasks[(size_t)(x % i)]);
+            }
+        }
+    }
     std::stable_sort(reduce.begin(), reduce.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
     for (auto& d : dual)
         std::stable_sort(d.begin(), d.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
@@ -796,6 +826,7 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
     a.gen = e->debug_fixed_gen ? 1u : e->gen;
     a.integrity = e->d_integrity;
     a.refine_min_pivot = e->refine_min_pivot;
+    a.extra_lds = e->debug_extra_lds;
     TimingRec rec{side, {nullptr, nullptr, nullptr}};
     if (e->timing) {
         for (auto& ev : rec.ev) {
@@ -833,7 +864,11 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
         a.col_ps = b.d_col_ps;
         a.amax = e->d_amax;
     }
-    HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.presplit, false));
+    a.queue = e->d_queue;
+    if (b.presplit && e->pipelined)
+        HIP_TRY(cfk::launch_solve_pc(e->kp, a, e->cu_count, e->stream));
+    else
+        HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.presplit, false));
     if (side_dual) HIP_TRY(hipStreamWaitEvent(e->side_stream, e->fork, 0));
     for (int c = 0; c < 3; ++c)
         if (dl.n[c] > 0) {

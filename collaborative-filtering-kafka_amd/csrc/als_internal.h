@@ -68,6 +68,8 @@ struct SolveArgs {
     int64_t rat_lo_off;     // presplit: words from the rh pairs to the rm pairs (nnz_padded / 2)
     const uint32_t* amax;   // presplit: bits of the opposite table's largest |x| (als_absmax): the split scale
     int64_t scratch_slabs;  // generic path: workgroup slabs in `partials` (its Gram when it does not fit in LDS)
+    int* queue;             // pipelined launch (als_solve_pc): next task index (zeroed by launch_solve_pc)
+    int32_t extra_lds;      // diagnostics (debug build's ALS_DEBUG_EXTRA_LDS, else 0): unused dynamic LDS per workgroup
 };
 // Factor row of local row `row` under the block's slot layout (wave-uniform: scalar arithmetic, once per task).
 __host__ __device__ inline int64_t factor_row(int64_t row_offset, int32_t rows_per_chunk, int64_t chunk_stride,
@@ -79,6 +81,9 @@ __host__ __device__ inline int64_t factor_row(int64_t row_offset, int32_t rows_p
 // Partial-slot integrity record (device, 4 words): [0] REDUCE tasks that found a bad slot, [1] generation, [2] slot,
 // [3] row of the first failure. Read back by every synchronising call of the engine.
 constexpr int INTEGRITY_WORDS = 4;
+// Slot value of an integrity record written by the pipelined launch (als_solve_pc) when a wave's hand-off wait ran
+// out of time (a protocol failure, not a partial slot).
+constexpr int32_t PC_TIMEOUT_SLOT = -2;
 // Diagnostic: skip the k x k solve after the Gram (stores the Gram diagonal instead) -- used by
 // tools/kbench.py to split a launch's time into Gram and solve. Only the debug build (CFK_DEBUG_KNOBS) can set
 // these flags; the product library never does.
@@ -122,6 +127,9 @@ hipError_t launch_generic(int precision, int kp, const SolveArgs& a, hipStream_t
 // same half).
 hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, bool presplit,
                         bool reduce);
+// Pipelined pre-split launch (als_solve_pc, kp 64 or 128): persistent, one workgroup per CU (cu_count), Gram waves
+// hand FULL systems to solver waves through LDS; same tasks and results as launch_solve(..., presplit = true, false).
+hipError_t launch_solve_pc(int kp, const SolveArgs& a, int cu_count, hipStream_t s);
 // Short rows in entry space (als_solve_dual): fp32 split path, kp 64 with cd 2, kp 128 with cd 2 or 4 (rows of
 // 16 * cd padded entries, i.e. cd / 2 blocks); `a.tasks` are FULL tasks of such rows.
 hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s);

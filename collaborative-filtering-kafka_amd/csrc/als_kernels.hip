@@ -22,7 +22,10 @@
 // into the factorisation; L is transposed once through the packed triangle for the backward substitution.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "als_internal.h"
 
@@ -383,6 +386,10 @@ __device__ __forceinline__ f32x4 mfma_f16(const u32x4& a, const u32x4& b, f32x4 
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
                                                   0);
 }
+// c + a.lo b.lo + a.hi b.hi on fp16 pairs (v_dot2_f32_f16; the fp16 x fp16 products are exact in fp32)
+__device__ __forceinline__ float dot2_f16(unsigned a, unsigned b, float c) {
+    return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, a), __builtin_bit_cast(f16x2, b), c, false);
+}
 // Scale exponent s of a pre-split table from the bits of its largest |x| (als_absmax): 2^s max|x| <= 2^14 < the fp16
 // maximum 65504 (no overflow at any rounding), and the table's values use the whole fp16 range (m stays normal for
 // |x| >= 2^-17 max|x|). A zero, infinite or NaN maximum keeps s = 0; s is clamped so 2^s and 2^-2s stay usable.
@@ -615,6 +622,18 @@ __host__ __device__ constexpr int la_item_I(int C, int P, int t) {   // -1: the 
 #ifndef CFK_PS64_WAVES
 #define CFK_PS64_WAVES 4
 #endif
+// Pipelined launch: the solver waves' issue priority (s_setprio) and their sweep column broadcasts (1: lane swaps,
+// the shorter latency; 0: ds_bpermute)
+#ifndef CFK_PC_PRIO
+#define CFK_PC_PRIO 1
+#endif
+#ifndef CFK_PC_SWAP
+#define CFK_PC_SWAP 0
+#endif
+// Gram waves of the 16-wave pipelined pre-split KP = 64 workgroup (the rest solve)
+#ifndef CFK_PC64_NG
+#define CFK_PC64_NG 12
+#endif
 #ifndef CFK_SOLVE_LOOKAHEAD
 #define CFK_SOLVE_LOOKAHEAD 1
 #endif
@@ -684,9 +703,10 @@ __device__ __forceinline__ int logical_entry(int q) {
 
 // Tag for solve_tiles' A0: keep NO copy of the system; a refinement step (rare: every Netflix-shape user row passes
 // the pivot gate, tools/refine_accuracy.py) forms its residual from the factor rows instead, r = b - D (G (D x) +
-// lambda n D x) with G z = sum_e y_e (y_e . z) over the row's entries -- the exact fp32 rows, so the step also
-// corrects the pre-split Gram's 2^-22 representation. Frees the copy's registers (4 waves per SIMD on the pre-split
-// KP = 64 path instead of 3).
+// lambda n D x) with G z = sum_e y_e (y_e . z) over the row's entries. G z uses the exact fp32 rows; b is the RHS
+// the Gram pass accumulated, which on the pre-split path comes from the split (h + m) values, so the step corrects
+// the Gram's 2^-22 representation error but not the RHS's. Frees the copy's registers (4 waves per SIMD on the
+// pre-split KP = 64 path instead of 3).
 struct RowResidual {
     __device__ __forceinline__ void put(int, const f32x4&) {}
 };
@@ -695,7 +715,7 @@ struct RowResidual {
 // DUAL: the system is the entry Gram of a short row (als_solve_dual): unknown 16b + j = the row's entry at
 // physical position 16b + j, real when that entry exists (padding entries get an identity row), and the
 // solution alpha goes to buf[16b + j] (read by the caller after a wave_sync) instead of a factor row.
-template <int C, bool DUAL = false, class TT, class KT>
+template <int C, bool DUAL = false, bool FORCE_SWAP = false, class TT, class KT>
 __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc)[C], float* buf, const Task& tk,
                                             const SolveArgs& a, int lane) {
     const int g = lane >> 4, j = lane & 15;
@@ -771,7 +791,7 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 
     // ---- factorisation (matrix part only) ----
     float nrd_min = -1.f;
-    constexpr bool SWAPC = 16 * C >= CFK_COL_SWAP;
+    constexpr bool SWAPC = FORCE_SWAP || 16 * C >= CFK_COL_SWAP;
     if constexpr (CFK_SOLVE_LOOKAHEAD) {
         {
             f32x4 S0 = T.get(tile_index<C>(0, 0));
@@ -1066,6 +1086,222 @@ __global__ __launch_bounds__(256) void als_pack_cols_ps(const int32_t* __restric
     dst[i] = col[(i & ~(int64_t)31) + k];
 }
 
+// A PARTIAL task's raw accumulators -> its partial slot ([word][lane], keyed words + check word, SlotCodec).
+template <int C>
+__device__ __forceinline__ void store_partial(const SolveArgs& a, const Task& tk, const MfmaAcc<C>& acc, int lane) {
+    using Acc = MfmaAcc<C>;
+    constexpr int SLOT_WORDS = Acc::NWORDS + 1;   // + integrity check word
+    float* dst = (float*)a.partials + (int64_t)tk.slot * (SLOT_WORDS * 64) + lane;
+    SlotCodec cd{slot_key(a.gen, tk.slot, lane)};
+#pragma unroll
+    for (int p = 0; p < Acc::NT; ++p)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[(p * 4 + r) * 64] = cd.enc(acc.g[p][r], p * 4 + r);
+#pragma unroll
+    for (int c = 0; c < C; ++c) dst[(Acc::NT * 4 + c) * 64] = cd.enc(acc.rhs[c], Acc::NT * 4 + c);
+    dst[Acc::NWORDS * 64] = cd.check_word<float>(Acc::NWORDS);
+}
+
+// Pre-split fp16 Gram of one FULL / PARTIAL task into acc (tiles, RHS) and E (the diagonal tiles' h m^T terms,
+// folded by the caller), in the table's units. img: the wave's 2 C KB LDS image (1-KB aligned); buf: its KP floats.
+// LEAN (the pipelined KP = 128 Gram role, whose wave has half the register file): E unused -- a diagonal tile takes
+// hh + hm + mh like the others (3 MFMAs) -- and the RHS by v_dot2_f32_f16 on the operand registers (the lane's h/m
+// pairs of its 8 entries times the rh/rm pairs, per-lane partial sums that solve_tiles' col_sum completes) instead
+// of 2 C RHS MFMA tiles: 32 + 24 accumulator registers fewer, 108 MFMAs per block at KP = 128 instead of 116.
+template <int KP, bool LEAN = false>
+__device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk, MfmaAcc<KP / 16>& acc,
+                                              f32x4 (&E)[KP / 16], unsigned char* img, float* buf, int lane) {
+    constexpr int C = KP / 16;
+    using Acc = MfmaAcc<C>;
+    constexpr int B = BLOCK_SUBSTEPS;
+    const int g = lane >> 4, j = lane & 15;
+    const int nblk = (tk.nsteps + B - 1) / B;
+    // Two-term fp16 Gram over a PRE-SPLIT opposite table (als_presplit, once per half: the scaled h/m fp16
+    // terms of every factor row, split2). Tile (b1, b2) takes hh + hm + mh (3 MFMAs), a diagonal tile hh + E
+    // with E = h m^T folded as E + E^T once per task (2 MFMAs). The RHS Y^T r is 2 MFMAs per feature block on
+    // B[k][c] = rh_k (columns 0-7) / rm_k (columns 8-15), r = rh + rm exact in fp16 for every Java short:
+    // column 0 + column 8 = Y_b^T r. KP = 64: 34 MFMAs per 32-entry block (the on-the-fly bf16 split: 52
+    // + VALU RHS); KP = 128: 116 (200 + VALU RHS).
+    static_assert(C == 4 || C == 8, "pre-split Gram: KP = 64 or 128");
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    constexpr int NPL = 2;                 // planes h, m
+    const char* tbase = (const char*)a.opp_split;
+    const int sc = split_exp(*a.amax);     // the table's scale 2^sc (wave-uniform scalar load)
+    constexpr int NR = LEAN ? 1 : C;       // RHS MFMA tiles (LEAN: none)
+    f32x4 racc[NR];
+#pragma unroll
+    for (int b = 0; b < NR; ++b) racc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float rsum[C];                         // LEAN: per-lane RHS partial sums
+#pragma unroll
+    for (int b = 0; b < C; ++b) rsum[b] = 0.f;
+    // the block's MFMAs on operands P[plane h/m][feature block b] (entries 8g..8g+7 of feature C j + b as
+    // fp16 pairs) and the fp16 rating pairs R of the same entries (rh or rm by the lane's column; LEAN: rh in R,
+    // rm in Rm, every lane)
+    auto mfma_block = [&](const u32x4 (&P)[NPL][C], const u32x4& R, const u32x4& Rm) {
+#pragma unroll
+        for (int b1 = 0; b1 < C; ++b1)
+#pragma unroll
+            for (int b2 = b1; b2 < C; ++b2) {
+                f32x4 t = acc.g[tile_index<C>(b1, b2)];
+                if (CFK_DIAG_SYM && !LEAN && b1 == b2) {
+                    E[b1] = mfma_f16(P[0][b1], P[1][b1], E[b1]);
+                } else {
+                    t = mfma_f16(P[0][b1], P[1][b2], t);
+                    t = mfma_f16(P[1][b1], P[0][b2], t);
+                }
+                t = mfma_f16(P[0][b1], P[0][b2], t);
+                acc.g[tile_index<C>(b1, b2)] = t;
+            }
+        if constexpr (LEAN) {
+#pragma unroll
+            for (int b = 0; b < C; ++b) {
+                float v = rsum[b];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    v = dot2_f16(P[1][b][w], Rm[w], v);
+                    v = dot2_f16(P[0][b][w], Rm[w], v);
+                    v = dot2_f16(P[1][b][w], R[w], v);
+                    v = dot2_f16(P[0][b][w], R[w], v);
+                }
+                rsum[b] = v;
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < C; ++b) {
+                f32x4 t = racc[b];
+                t = mfma_f16(P[1][b], R, t);
+                t = mfma_f16(P[0][b], R, t);
+                racc[b] = t;
+            }
+        }
+        MFMA_DRAIN();
+    };
+    // LDS image of one 32-entry block per wave (2 C KB: 8 KB at KP = 64, 16 KB at KP = 128): 2 C LDS-DMA
+    // instructions (plane pl, 128-B plane half ph, entry quarter m) of 1 KB, instruction = 8 rows x one
+    // 128-B half plane, lane 8 r + i holding 16-B chunk i ^ 2 (r >> 1) of the row of entry
+    // k = 16 (m >> 1) + 8 (r >> 2) + 4 (m & 1) + (r & 3): whole cache lines per row for the address unit (8
+    // lines per instruction), and a chunk swizzle that makes the transposed reads conflict-free. Operand
+    // (pl, b) of lane (g, 4 q + p) = two ds_read_b64_tr_b16 (h = 0, 1: entries 8 g + 4 h + 0..3), lane
+    // 4 q + p addressing entry 8 g + 4 h + q, plane positions 16 b + 4 p .. + 3 (features C j + b,
+    // j = 4 p .. 4 p + 3); the 16 lanes of a group receive features j = 0..15 of their 4 entries: exactly
+    // the MFMA A/B operand, no lane movement.
+    typedef short s16x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) void lds_void;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    constexpr int NH = C / 4;              // 128-B halves per plane
+    const int r8 = lane >> 3;
+    const uint32_t ld_off = 16u * (uint32_t)((lane & 7) ^ (2 * (r8 >> 1)));
+    const int q = (lane >> 2) & 3, p = lane & 3, rr = 4 * (g & 1) + q;
+    uint32_t rd[4];   // per feature block b & 3 (the 128-B half b >> 2 is an immediate)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        rd[b] = 2048u * (uint32_t)(g >> 1) + 16u * (uint32_t)(8 * rr + ((2 * b + (p >> 1)) ^ (2 * (rr >> 1)))) +
+                8u * (uint32_t)(p & 1);
+    // per-plane table bases kept in SGPRs (opaque to the optimiser: folded into the per-lane offset they
+    // would force 64-bit addresses; an LDS-DMA takes no immediate offset here, it would move the LDS
+    // destination too), so every DMA takes the saddr form with one 32-bit lane offset per row
+    const char* tpl[NPL * NH];
+#pragma unroll
+    for (int x = 0; x < NPL * NH; ++x) {
+        tpl[x] = tbase + (x / NH) * 2 * KP + (x % NH) * 128;
+        asm volatile("" : "+s"(tpl[x]));
+    }
+    auto issue = [&](const i32x4& cv) {
+        static_for<0, 4>([&](auto M_) {
+            constexpr int m = decltype(M_)::value;
+            // 24-bit multiply: pre-split tables are host-checked < 2^24 rows and < 4 GiB
+            const uint32_t vo = __umul24((uint32_t)cv[m], (uint32_t)presplit_row_bytes(KP)) + ld_off;
+            static_for<0, NPL * NH>([&](auto X_) {
+                constexpr int x = decltype(X_)::value;   // plane x / NH, half x % NH
+                __builtin_amdgcn_global_load_lds((const void*)(tpl[x] + vo),
+                                                 (lds_void*)(img + (x * 4 + m) * 1024), 16, 0, 0);
+            });
+        });
+    };
+    auto read1 = [&](auto PL_, auto B_) {
+        constexpr int pl = decltype(PL_)::value, b = decltype(B_)::value;
+        u32x4 P;
+        static_for<0, 2>([&](auto H_) {
+            constexpr int h = decltype(H_)::value;
+            const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_s16x4*)(img + rd[b & 3] + ((pl * NH + (b >> 2)) * 4 + h) * 1024));
+            const u32x2 w = __builtin_bit_cast(u32x2, v);
+            P[2 * h] = w[0];
+            P[2 * h + 1] = w[1];
+        });
+        return P;
+    };
+    auto read = [&](u32x4 (&P)[NPL][C]) {
+        static_for<0, NPL>([&](auto PL_) {
+            static_for<0, C>([&](auto B_) { P[decltype(PL_)::value][decltype(B_)::value] = read1(PL_, B_); });
+        });
+    };
+    if (nblk > 0) {
+        const int lastb = nblk - 1;
+        const i32x4* cp = (const i32x4*)(a.col_ps + tk.begin) + r8;          // + 8 per block
+        // rating pairs of the lane's column half: rh (columns 0-7) or rm (columns 8-15); LEAN: rh, and rm in Rmn
+        const u32x4* rp = (const u32x4*)(a.rat_pk + ((j >= 8 && !LEAN) ? a.rat_lo_off : 0) + (tk.begin >> 1)) + g;
+        const u32x4* rpm = (const u32x4*)(a.rat_pk + a.rat_lo_off + (tk.begin >> 1)) + g;
+        i32x4 cv = cp[0];
+        u32x4 Rn = rp[0], Rmn = {0u, 0u, 0u, 0u};
+        if constexpr (LEAN) Rmn = rpm[0];
+        issue(cv);
+        cv = cp[8 * min(1, lastb)];
+        for (int b = 0; b < nblk; ++b) {
+            const u32x4 R = Rn, Rm = Rmn;
+            // every vector-memory op of this wave done: this block's LDS-DMA (and the column / rating loads
+            // the DMA issue and the MFMAs below need anyway) -- explicit, not left to the compiler's tracking
+            // of LDS-DMA writes (tests/test_isa_guard.py checks it)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            u32x4 P[NPL][C];
+            read(P);
+            // the operands are in registers before the image is overwritten by the next block's DMA
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (b < lastb) issue(cv);
+            cv = cp[8 * min(b + 2, lastb)];
+            Rn = rp[4 * min(b + 1, lastb)];
+            if constexpr (LEAN) Rmn = rpm[4 * min(b + 1, lastb)];
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_block(P, R, Rm);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // back to the table's units: the Gram terms by 2^-2sc, the RHS by 2^-sc (powers of two: exact)
+#pragma unroll
+    for (int t = 0; t < Acc::NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc.g[t][r] = ldexpf(acc.g[t][r], -2 * sc);
+    if constexpr (LEAN) {   // the other paths' per-lane RHS layout: the whole sum in row g = 0, zeros elsewhere
+#pragma unroll
+        for (int b = 0; b < C; ++b) {
+            const float v = ldexpf(col_sum(rsum[b]), -sc);
+            acc.rhs[b] = (g == 0) ? v : 0.f;
+        }
+        return;
+    }
+#pragma unroll
+    for (int b = 0; b < C; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) E[b][r] = ldexpf(E[b][r], -2 * sc);
+    // RHS tiles (row i of block b = feature C i + b; column 0 = Y^T rh, column 8 = Y^T rm) -> the per-lane
+    // partial layout of the other paths: lane (0, j) holds feature C j + b, the other rows zero (col_sum
+    // restores it)
+    wave_sync();
+#pragma unroll
+    for (int b = 0; b < NR; ++b) {
+        f32x4 v = racc[b];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)   // lane (g, 8) += lane (g, 0): DPP row_shr:8
+            v[r] = ldexpf(v[r] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[r]), 0x118,
+                                                                            0xf, 0xf, false)), -sc);
+        if (j == 8) *(f32x4*)(buf + 16 * b + 4 * g) = v;
+    }
+    wave_sync();
+#pragma unroll
+    for (int b = 0; b < C; ++b) acc.rhs[b] = (g == 0) ? buf[16 * b + j] : 0.f;
+    wave_sync();
+}
+
 // REDUCE = true: the launch of a half's REDUCE tasks (sum of partial slots + solve), compiled apart from the
 // gather kernel so neither carries the other's code and registers.
 template <int KP, int MINW, bool SPLIT, bool PRESPLIT = false, bool REDUCE = false>
@@ -1173,162 +1409,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             for (int c = 0; c < C; ++c) acc.rhs[c] += r * y[c];
         };
         if constexpr (PRESPLIT) {
-            // Two-term fp16 Gram over a PRE-SPLIT opposite table (als_presplit, once per half: the scaled h/m fp16
-            // terms of every factor row, split2). Tile (b1, b2) takes hh + hm + mh (3 MFMAs), a diagonal tile hh + E
-            // with E = h m^T folded as E + E^T once per task (2 MFMAs). The RHS Y^T r is 2 MFMAs per feature block on
-            // B[k][c] = rh_k (columns 0-7) / rm_k (columns 8-15), r = rh + rm exact in fp16 for every Java short:
-            // column 0 + column 8 = Y_b^T r. KP = 64: 34 MFMAs per 32-entry block (the on-the-fly bf16 split: 52
-            // + VALU RHS); KP = 128: 116 (200 + VALU RHS).
-            static_assert(C == 4 || C == 8, "pre-split Gram: KP = 64 or 128");
-            typedef int i32x4 __attribute__((ext_vector_type(4)));
-            constexpr int NPL = 2;                 // planes h, m
-            const char* tbase = (const char*)a.opp_split;
-            const int sc = split_exp(*a.amax);     // the table's scale 2^sc (wave-uniform scalar load)
-            f32x4 racc[C];
-#pragma unroll
-            for (int b = 0; b < C; ++b) racc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-            // the block's MFMAs on operands P[plane h/m][feature block b] (entries 8g..8g+7 of feature C j + b as
-            // fp16 pairs) and the fp16 rating pairs R of the same entries (rh or rm by the lane's column)
-            auto mfma_block = [&](const u32x4 (&P)[NPL][C], const u32x4& R) {
-#pragma unroll
-                for (int b1 = 0; b1 < C; ++b1)
-#pragma unroll
-                    for (int b2 = b1; b2 < C; ++b2) {
-                        f32x4 t = acc.g[tile_index<C>(b1, b2)];
-                        if (CFK_DIAG_SYM && b1 == b2) {
-                            E[b1] = mfma_f16(P[0][b1], P[1][b1], E[b1]);
-                        } else {
-                            t = mfma_f16(P[0][b1], P[1][b2], t);
-                            t = mfma_f16(P[1][b1], P[0][b2], t);
-                        }
-                        t = mfma_f16(P[0][b1], P[0][b2], t);
-                        acc.g[tile_index<C>(b1, b2)] = t;
-                    }
-#pragma unroll
-                for (int b = 0; b < C; ++b) {
-                    f32x4 t = racc[b];
-                    t = mfma_f16(P[1][b], R, t);
-                    t = mfma_f16(P[0][b], R, t);
-                    racc[b] = t;
-                }
-                MFMA_DRAIN();
-            };
-            // LDS image of one 32-entry block per wave (2 C KB: 8 KB at KP = 64, 16 KB at KP = 128): 2 C LDS-DMA
-            // instructions (plane pl, 128-B plane half ph, entry quarter m) of 1 KB, instruction = 8 rows x one
-            // 128-B half plane, lane 8 r + i holding 16-B chunk i ^ 2 (r >> 1) of the row of entry
-            // k = 16 (m >> 1) + 8 (r >> 2) + 4 (m & 1) + (r & 3): whole cache lines per row for the address unit (8
-            // lines per instruction), and a chunk swizzle that makes the transposed reads conflict-free. Operand
-            // (pl, b) of lane (g, 4 q + p) = two ds_read_b64_tr_b16 (h = 0, 1: entries 8 g + 4 h + 0..3), lane
-            // 4 q + p addressing entry 8 g + 4 h + q, plane positions 16 b + 4 p .. + 3 (features C j + b,
-            // j = 4 p .. 4 p + 3); the 16 lanes of a group receive features j = 0..15 of their 4 entries: exactly
-            // the MFMA A/B operand, no lane movement.
-            typedef short s16x4 __attribute__((ext_vector_type(4)));
-            typedef __attribute__((address_space(3))) void lds_void;
-            typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-            constexpr int NH = C / 4;              // 128-B halves per plane
-            constexpr int IMG = NPL * C * 1024;
-            static_assert(sizeof(stage_lds[0]) >= IMG, "stage image");
-            unsigned char* img = stage_lds[uni(wave)];
-            const int r8 = lane >> 3;
-            const uint32_t ld_off = 16u * (uint32_t)((lane & 7) ^ (2 * (r8 >> 1)));
-            const int q = (lane >> 2) & 3, p = lane & 3, rr = 4 * (g & 1) + q;
-            uint32_t rd[4];   // per feature block b & 3 (the 128-B half b >> 2 is an immediate)
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                rd[b] = 2048u * (uint32_t)(g >> 1) + 16u * (uint32_t)(8 * rr + ((2 * b + (p >> 1)) ^ (2 * (rr >> 1)))) +
-                        8u * (uint32_t)(p & 1);
-            // per-plane table bases kept in SGPRs (opaque to the optimiser: folded into the per-lane offset they
-            // would force 64-bit addresses; an LDS-DMA takes no immediate offset here, it would move the LDS
-            // destination too), so every DMA takes the saddr form with one 32-bit lane offset per row
-            const char* tpl[NPL * NH];
-#pragma unroll
-            for (int x = 0; x < NPL * NH; ++x) {
-                tpl[x] = tbase + (x / NH) * 2 * KP + (x % NH) * 128;
-                asm volatile("" : "+s"(tpl[x]));
-            }
-            auto issue = [&](const i32x4& cv) {
-                static_for<0, 4>([&](auto M_) {
-                    constexpr int m = decltype(M_)::value;
-                    // 24-bit multiply: pre-split tables are host-checked < 2^24 rows and < 4 GiB
-                    const uint32_t vo = __umul24((uint32_t)cv[m], (uint32_t)presplit_row_bytes(KP)) + ld_off;
-                    static_for<0, NPL * NH>([&](auto X_) {
-                        constexpr int x = decltype(X_)::value;   // plane x / NH, half x % NH
-                        __builtin_amdgcn_global_load_lds((const void*)(tpl[x] + vo),
-                                                         (lds_void*)(img + (x * 4 + m) * 1024), 16, 0, 0);
-                    });
-                });
-            };
-            auto read1 = [&](auto PL_, auto B_) {
-                constexpr int pl = decltype(PL_)::value, b = decltype(B_)::value;
-                u32x4 P;
-                static_for<0, 2>([&](auto H_) {
-                    constexpr int h = decltype(H_)::value;
-                    const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (lds_s16x4*)(img + rd[b & 3] + ((pl * NH + (b >> 2)) * 4 + h) * 1024));
-                    const u32x2 w = __builtin_bit_cast(u32x2, v);
-                    P[2 * h] = w[0];
-                    P[2 * h + 1] = w[1];
-                });
-                return P;
-            };
-            auto read = [&](u32x4 (&P)[NPL][C]) {
-                static_for<0, NPL>([&](auto PL_) {
-                    static_for<0, C>([&](auto B_) { P[decltype(PL_)::value][decltype(B_)::value] = read1(PL_, B_); });
-                });
-            };
-            if (nblk > 0) {
-                const int lastb = nblk - 1;
-                const i32x4* cp = (const i32x4*)(a.col_ps + tk.begin) + r8;          // + 8 per block
-                // rating pairs of the lane's column half: rh (columns 0-7) or rm (columns 8-15)
-                const u32x4* rp = (const u32x4*)(a.rat_pk + (j >= 8 ? a.rat_lo_off : 0) + (tk.begin >> 1)) + g;
-                i32x4 cv = cp[0];
-                u32x4 Rn = rp[0];
-                issue(cv);
-                cv = cp[8 * min(1, lastb)];
-                for (int b = 0; b < nblk; ++b) {
-                    const u32x4 R = Rn;
-                    // every vector-memory op of this wave done: this block's LDS-DMA (and the column / rating loads
-                    // the DMA issue and the MFMAs below need anyway) -- explicit, not left to the compiler's tracking
-                    // of LDS-DMA writes (tests/test_isa_guard.py checks it)
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    u32x4 P[NPL][C];
-                    read(P);
-                    // the operands are in registers before the image is overwritten by the next block's DMA
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    if (b < lastb) issue(cv);
-                    cv = cp[8 * min(b + 2, lastb)];
-                    Rn = rp[4 * min(b + 1, lastb)];
-                    __builtin_amdgcn_sched_barrier(0);
-                    mfma_block(P, R);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            // back to the table's units: the Gram terms by 2^-2sc, the RHS by 2^-sc (powers of two: exact)
-#pragma unroll
-            for (int t = 0; t < Acc::NT; ++t)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) acc.g[t][r] = ldexpf(acc.g[t][r], -2 * sc);
-#pragma unroll
-            for (int b = 0; b < C; ++b)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) E[b][r] = ldexpf(E[b][r], -2 * sc);
-            // RHS tiles (row i of block b = feature C i + b; column 0 = Y^T rh, column 8 = Y^T rm) -> the per-lane
-            // partial layout of the other paths: lane (0, j) holds feature C j + b, the other rows zero (col_sum
-            // restores it)
-            wave_sync();
-#pragma unroll
-            for (int b = 0; b < C; ++b) {
-                f32x4 v = racc[b];
-#pragma unroll
-                for (int r = 0; r < 4; ++r)   // lane (g, 8) += lane (g, 0): DPP row_shr:8
-                    v[r] = ldexpf(v[r] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[r]), 0x118,
-                                                                                    0xf, 0xf, false)), -sc);
-                if (j == 8) *(f32x4*)(buf + 16 * b + 4 * g) = v;
-            }
-            wave_sync();
-#pragma unroll
-            for (int b = 0; b < C; ++b) acc.rhs[b] = (g == 0) ? buf[16 * b + j] : 0.f;
-            wave_sync();
+            gram_presplit<KP>(a, tk, acc, E, stage_lds[uni(wave)], buf, lane);
         } else if constexpr (SPLIT) {
             // Split-bf16 Gram: one v_mfma_f32_16x16x32_bf16 consumes a whole 32-entry block. Lane (g, j)
             // holds A[i = j][k = 8g + t] = y_t[C*j + b] (its own gathered piece, component b, entry t of its
@@ -1661,15 +1742,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
     }
 
     if (!REDUCE && tk.kind == TASK_PARTIAL) {
-        float* dst = part + (int64_t)tk.slot * (SLOT_WORDS * 64) + lane;
-        SlotCodec cd{slot_key(a.gen, tk.slot, lane)};
-#pragma unroll
-        for (int p = 0; p < Acc::NT; ++p)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) dst[(p * 4 + r) * 64] = cd.enc(acc.g[p][r], p * 4 + r);
-#pragma unroll
-        for (int c = 0; c < C; ++c) dst[(Acc::NT * 4 + c) * 64] = cd.enc(acc.rhs[c], Acc::NT * 4 + c);
-        dst[Acc::NWORDS * 64] = cd.check_word<float>(Acc::NWORDS);
+        store_partial<C>(a, tk, acc, lane);
         return;
     }
 
@@ -1695,6 +1768,246 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
         RegTiles<C> T{acc.g};
         RegStore<C> A0;
         solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Pipelined pre-split launch: Gram waves hand finished systems to solver waves through LDS
+// ---------------------------------------------------------------------------------------------------
+// One persistent workgroup per CU with NG Gram waves and NS solver waves (the hot path of the k = 64 user half and
+// of both halves at k = 128). Waves 0..NG-1 take FULL / PARTIAL tasks from a device queue (one vector atomic per
+// task on a.queue, zeroed before the launch; tasks stay longest first) and run the pre-split Gram (gram_presplit);
+// a PARTIAL task stores its partial slot as in als_solve_mfma, a FULL task's Gram tiles (accumulator layout,
+// [tile][lane][4]), RHS and task index go to a free hand-off slot in LDS. Waves NG.. take filled slots and run the
+// tile solve (solve_tiles with RowResidual) and store the factor row: the same arithmetic in the same order as
+// als_solve_mfma<KP, W, true, true>, so bitwise-equal results. The roles never hold each other's state, so each
+// fits its share of the register file -- at KP = 128 two waves per SIMD (one Gram, one solver) instead of the
+// one-kernel path's single wave holding both -- and the solve's latency-bound pivot chains run beside the Gram's
+// gathers and MFMAs instead of after them.
+// Slot protocol (LDS, workgroup scope): FREE -(Gram CAS)-> WRITING -(release store)-> FULL -(solver CAS)->
+// READING -(release store once its reads are in registers)-> FREE. A Gram wave waits only for a FREE slot, a
+// solver only for a FULL slot or the end (all Gram waves counted done, each after its last publish): no wait
+// cycle. Every wait is bounded in time (PC_WAIT_TICKS of the 100 MHz real-time counter); a wave that runs out
+// records it in the integrity record (slot PC_TIMEOUT_SLOT) and leaves, so the grid always drains.
+constexpr int PC_FREE = 0, PC_WRITING = 1, PC_FULL = 2, PC_READING = 3;
+constexpr uint64_t PC_WAIT_TICKS = 200000000ull;   // 2 s
+__device__ __forceinline__ uint64_t pc_now() { return __builtin_amdgcn_s_memrealtime(); }
+
+// LDS of the pipelined launch: dynamic (pc_smem), so that the solver role -- a separate, not inlined function --
+// addresses the same LDS objects as the kernel: per Gram wave a 2 C KB LDS-DMA image, per wave KP floats of solve
+// scratch, NSLOT hand-off slots (Gram tiles [tile][lane][4], RHS [16 C], task index), the slot states, the
+// count of finished Gram waves.
+extern __shared__ __attribute__((aligned(1024))) unsigned char pc_smem[];
+template <int KP, int NG, int NS, int NSLOT>
+struct PcLds {
+    static constexpr int C = KP / 16;
+    static constexpr int NT = MfmaAcc<C>::NT;
+    static constexpr int IMG_BYTES = 2 * C * 1024;
+    static constexpr int SBUF_OFF = NG * IMG_BYTES;
+    static constexpr int SLOT_OFF = SBUF_OFF + (NG + NS) * KP * 4;
+    static constexpr int SLOT_BYTES = NT * 1024 + 16 * C * 4 + 16;   // tiles, RHS, task index (+ pad)
+    static constexpr int STATE_OFF = SLOT_OFF + NSLOT * SLOT_BYTES;
+    static constexpr int BYTES = STATE_OFF + 4 * (NSLOT + 1);         // + ndone
+    static_assert(BYTES <= 160 * 1024, "pipelined launch: LDS");
+    static __device__ __forceinline__ unsigned char* img(int w) { return pc_smem + w * IMG_BYTES; }
+    static __device__ __forceinline__ float* sbuf(int w) { return (float*)(pc_smem + SBUF_OFF + w * KP * 4); }
+    static __device__ __forceinline__ float* slot(int i) { return (float*)(pc_smem + SLOT_OFF + i * SLOT_BYTES); }
+    static __device__ __forceinline__ int* state() { return (int*)(pc_smem + STATE_OFF); }
+};
+
+// The launch's arguments as wave-uniform values (readfirstlane of every field): inside a called function they
+// arrive in memory/VGPRs, and the solve branches on them and forms its addresses from them.
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+    return ((int64_t)uni((int)(v >> 32)) << 32) | (int64_t)(uint32_t)uni((int)(uint32_t)v);
+}
+template <class P>
+__device__ __forceinline__ P unip(P v) { return (P)uni64((int64_t)(uintptr_t)v); }
+__device__ __forceinline__ float unif(float v) { return __int_as_float(uni(__float_as_int(v))); }
+__device__ __forceinline__ SolveArgs uniform_args(const SolveArgs& in) {
+    SolveArgs a = in;
+    a.tasks = unip(in.tasks);
+    a.n_tasks = uni(in.n_tasks);
+    a.k = uni(in.k);
+    a.col = unip(in.col);
+    a.rat = unip(in.rat);
+    a.opp = unip(in.opp);
+    a.out = unip(in.out);
+    a.row_offset = uni64(in.row_offset);
+    a.partials = unip(in.partials);
+    a.lambda = unif(in.lambda);
+    a.sentinel = uni(in.sentinel);
+    a.flags = uni(in.flags);
+    a.opp_split = unip(in.opp_split);
+    a.gen = (uint32_t)uni((int)in.gen);
+    a.integrity = unip(in.integrity);
+    a.refine_min_pivot = unif(in.refine_min_pivot);
+    a.rat_pk = unip(in.rat_pk);
+    a.col_ps = unip(in.col_ps);
+    a.rows_per_chunk = uni(in.rows_per_chunk);
+    a.chunk_stride = uni64(in.chunk_stride);
+    a.rat_lo_off = uni64(in.rat_lo_off);
+    a.amax = unip(in.amax);
+    a.scratch_slabs = uni64(in.scratch_slabs);
+    a.queue = unip(in.queue);
+    a.extra_lds = uni(in.extra_lds);
+    return a;
+}
+
+// Solver role of als_solve_pc: one filled hand-off slot -> registers (then the slot is released) -> tile solve ->
+// factor row. Not inlined: as a call, the solve's registers are allocated for the solve alone; inlined into the
+// persistent loop the allocator kept loop-wide values live through it and spilled ~100 VGPRs at KP = 128.
+template <int KP, int NG, int NS, int NSLOT>
+__device__ __attribute__((noinline)) void pc_solve_slot(SolveArgs a_in, int sl_in, int wave_in) {
+    using L = PcLds<KP, NG, NS, NSLOT>;
+    constexpr int C = KP / 16;
+    using Acc = MfmaAcc<C>;
+    const SolveArgs a = uniform_args(a_in);
+    const int sl = uni(sl_in), wave = uni(wave_in);
+    const int lane = __lane_id(), g = lane >> 4, j = lane & 15;
+    const float* sp = L::slot(sl);
+    Acc acc;
+#pragma unroll
+    for (int p = 0; p < Acc::NT; ++p) acc.g[p] = *(const f32x4*)(sp + p * 256 + 4 * lane);
+#pragma unroll
+    for (int b = 0; b < C; ++b) acc.rhs[b] = (g == 0) ? sp[Acc::NT * 256 + 16 * b + j] : 0.f;
+    const int t = uni(((const int*)sp)[Acc::NT * 256 + 16 * C]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot is in registers: release it
+    if (lane == 0) __hip_atomic_store(L::state() + sl, PC_FREE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const Task tk = load_task(a.tasks + t);
+    if (a.flags & SOLVE_FLAG_SKIP_SOLVE) {   // diagnostics (kbench): Gram only
+        float* out = (float*)a.out + factor_row(a.row_offset, a.rows_per_chunk, a.chunk_stride, tk.row) * (int64_t)KP;
+        if (lane < 16) {
+#pragma unroll
+            for (int b = 0; b < C; ++b) out[C * lane + b] = acc.g[tile_index<C>(b, b)][0] + acc.rhs[b];
+        }
+        return;
+    }
+    RegTiles<C> T{acc.g};
+    RowResidual A0;
+    solve_tiles<C, false, CFK_PC_SWAP != 0>(T, A0, acc.rhs, L::sbuf(wave), tk, a, lane);
+}
+
+template <int KP, int NG, int NS, int NSLOT>
+__global__ __launch_bounds__(64 * (NG + NS), 1) void als_solve_pc(SolveArgs a) {
+    using L = PcLds<KP, NG, NS, NSLOT>;
+    constexpr int C = KP / 16;
+    using Acc = MfmaAcc<C>;
+    constexpr auto WG = __HIP_MEMORY_SCOPE_WORKGROUP;
+    int* state = L::state();
+    int* ndone = state + NSLOT;
+
+    const int wave = uni((int)(threadIdx.x >> 6)), lane0 = threadIdx.x & 63;
+    if (threadIdx.x < NSLOT) state[threadIdx.x] = PC_FREE;
+    if (threadIdx.x == 0) *ndone = 0;
+    __syncthreads();   // the only workgroup barrier: every wave passes it before any wave waits on another
+
+#if defined(CFK_PC_ROLE_TEST) && CFK_PC_ROLE_TEST == 2
+    if (wave < NG) return;
+#endif
+    if (wave < NG) {
+        // ---- Gram role ----
+        unsigned char* img = L::img(wave);
+        float* buf = L::sbuf(wave);
+        int tl = 0;
+        if (lane0 == 0) tl = atomicAdd(a.queue, 1);
+        int t = uni(tl);
+        while (t < a.n_tasks) {
+            // a fresh lane id per task: nothing lane-derived is hoisted out of the loop and kept live across it
+            const int lane = opaque(lane0);
+            int tn = 0;   // the next task index, fetched under this task's Gram
+            if (lane == 0) tn = atomicAdd(a.queue, 1);
+            const Task tk = load_task(a.tasks + t);
+            Acc acc;
+#pragma unroll
+            for (int p = 0; p < Acc::NT; ++p) acc.g[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc.rhs[c] = 0.f;
+            f32x4 E[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) E[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+            constexpr bool LEAN = KP == 128;
+            gram_presplit<KP, LEAN>(a, tk, acc, E, img, buf, lane);
+            if constexpr (CFK_DIAG_SYM && !LEAN) fold_diag<C>(acc, E, lane);
+            if (tk.kind == TASK_PARTIAL) {
+                store_partial<C>(a, tk, acc, lane);
+            } else {
+                // claim a FREE slot
+                int sl = -1;
+                const uint64_t t0 = pc_now();
+                while (true) {
+                    int cl = -1;
+                    if (lane == 0) {
+                        for (int i = 0; i < NSLOT; ++i) {
+                            int expct = PC_FREE;
+                            if (__hip_atomic_load(&state[i], __ATOMIC_RELAXED, WG) == PC_FREE &&
+                                __hip_atomic_compare_exchange_strong(&state[i], &expct, PC_WRITING, __ATOMIC_ACQUIRE,
+                                                                     __ATOMIC_RELAXED, WG)) {
+                                cl = i;
+                                break;
+                            }
+                        }
+                    }
+                    sl = uni(cl);
+                    if (sl >= 0 || pc_now() - t0 > PC_WAIT_TICKS) break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (sl < 0) {   // no solver freed a slot in PC_WAIT_TICKS: record and leave (the grid drains)
+                    report_bad_slot(a.integrity, a.gen, PC_TIMEOUT_SLOT, tk.row, true, lane);
+                    break;
+                }
+                float* sp = L::slot(sl);
+#pragma unroll
+                for (int p = 0; p < Acc::NT; ++p) *(f32x4*)(sp + p * 256 + 4 * lane) = acc.g[p];
+                const int g = lane >> 4, j = lane & 15;
+                if (g == 0) {
+#pragma unroll
+                    for (int b = 0; b < C; ++b) sp[Acc::NT * 256 + 16 * b + j] = acc.rhs[b];
+                }
+                if (lane == 0) {
+                    ((int*)sp)[Acc::NT * 256 + 16 * C] = t;
+                    __hip_atomic_store(&state[sl], PC_FULL, __ATOMIC_RELEASE, WG);
+                }
+            }
+            t = uni(tn);
+        }
+        if (lane0 == 0) __hip_atomic_fetch_add(ndone, 1, __ATOMIC_RELEASE, WG);
+        return;
+    }
+
+    // ---- solver role ----
+#if defined(CFK_PC_ROLE_TEST) && CFK_PC_ROLE_TEST == 1
+    return;
+#endif
+    // the solve is a latency-bound chain beside a Gram wave with independent MFMAs to spare: it issues first
+    if constexpr (CFK_PC_PRIO > 0) __builtin_amdgcn_s_setprio(CFK_PC_PRIO);
+    uint64_t t0 = pc_now();
+    while (true) {
+        int cl = -1, fin = 0;
+        if (lane0 == 0) {
+            const int nd = __hip_atomic_load(ndone, __ATOMIC_ACQUIRE, WG);   // before the scan: see the publishes
+            for (int i = 0; i < NSLOT; ++i) {
+                int expct = PC_FULL;
+                if (__hip_atomic_load(&state[i], __ATOMIC_RELAXED, WG) == PC_FULL &&
+                    __hip_atomic_compare_exchange_strong(&state[i], &expct, PC_READING, __ATOMIC_ACQUIRE,
+                                                         __ATOMIC_RELAXED, WG)) {
+                    cl = i;
+                    break;
+                }
+            }
+            fin = cl < 0 && nd == NG;
+        }
+        const int sl = uni(cl);
+        if (uni(fin)) break;
+        if (sl < 0) {
+            if (pc_now() - t0 > PC_WAIT_TICKS) {   // no Gram wave published or finished in PC_WAIT_TICKS
+                report_bad_slot(a.integrity, a.gen, PC_TIMEOUT_SLOT, -1, true, lane0);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        pc_solve_slot<KP, NG, NS, NSLOT>(a, sl, wave);
+        t0 = pc_now();
     }
 }
 
@@ -2136,6 +2449,31 @@ __global__ __launch_bounds__(256) void als_predict_generic(const T* __restrict__
 
 int blocks_for(int n_tasks) { return (n_tasks + WAVES - 1) / WAVES; }
 
+// hipFuncAttributeMaxDynamicSharedMemorySize of one kernel on the current device, raised to `bytes` when a launch
+// needs more than was set there before (engines of several devices and host threads launch concurrently: the
+// per-(kernel, device) high-water mark is kept under a lock).
+hipError_t ensure_dyn_lds(const void* fn, int bytes) {
+    constexpr int MAXDEV = 64;
+    static std::mutex mu;
+    static std::vector<std::pair<const void*, std::vector<int>>> tab;   // per kernel: bytes set per device
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= MAXDEV) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> g(mu);
+    std::vector<int>* set = nullptr;
+    for (auto& x : tab)
+        if (x.first == fn) set = &x.second;
+    if (!set) {
+        tab.emplace_back(fn, std::vector<int>(MAXDEV, 0));
+        set = &tab.back().second;
+    }
+    if (bytes <= (*set)[dev]) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) (*set)[dev] = bytes;
+    return e;
+}
+
 template <class T, int KP, Path P, int MINW = 1, bool PRESPLIT = false>
 hipError_t launch_solve_t(const SolveArgs& a, hipStream_t s, bool reduce) {
     if (a.n_tasks <= 0) return hipSuccess;
@@ -2144,18 +2482,14 @@ hipError_t launch_solve_t(const SolveArgs& a, hipStream_t s, bool reduce) {
         static_assert(std::is_same<T, float>::value, "MFMA paths are fp32");
         constexpr int nw = mfma_waves<KP>();
         const unsigned grid = (unsigned)((a.n_tasks + nw - 1) / nw);
+        const size_t dyn = (size_t)a.extra_lds;   // debug build only: unused LDS per workgroup (occupancy sweeps)
         if (reduce)   // one REDUCE kernel per KP: the partial slots have the same layout on every Gram path
             als_solve_mfma<KP, MINW, false, false, true><<<grid, 64 * nw, 0, s>>>(a);
         else
-            als_solve_mfma<KP, MINW, P == Path::MFMA_SPLIT, PRESPLIT><<<grid, 64 * nw, 0, s>>>(a);
+            als_solve_mfma<KP, MINW, P == Path::MFMA_SPLIT, PRESPLIT><<<grid, 64 * nw, dyn, s>>>(a);
     } else {
-        static bool attr = false;
-        if (!attr) {
-            hipError_t e = hipFuncSetAttribute((const void*)als_solve_valu<T, KP>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-            if (e != hipSuccess) return e;
-            attr = true;
-        }
+        hipError_t e = ensure_dyn_lds((const void*)als_solve_valu<T, KP>, bytes);
+        if (e != hipSuccess) return e;
         als_solve_valu<T, KP><<<blocks_for(a.n_tasks), 256, bytes, s>>>(a);
     }
     return hipGetLastError();
@@ -2281,6 +2615,31 @@ hipError_t launch_pack_cols_ps(const int32_t* col, int32_t* dst, int64_t n_entri
     return hipGetLastError();
 }
 
+template <int KP, int NG, int NS, int NSLOT>
+hipError_t launch_pc_t(const SolveArgs& a, int cu_count, hipStream_t s) {
+    using L = PcLds<KP, NG, NS, NSLOT>;
+    hipError_t e = ensure_dyn_lds((const void*)als_solve_pc<KP, NG, NS, NSLOT>, L::BYTES);
+    if (e != hipSuccess) return e;
+    const unsigned grid = (unsigned)std::min<int64_t>(cu_count, ((int64_t)a.n_tasks + NG - 1) / NG);
+    als_solve_pc<KP, NG, NS, NSLOT><<<grid, 64 * (NG + NS), L::BYTES, s>>>(a);
+    return hipGetLastError();
+}
+// Pipelined pre-split launch (als_solve_pc): grid = min(CUs, enough workgroups for the tasks); a.queue zeroed here.
+hipError_t launch_solve_pc(int kp, const SolveArgs& a, int cu_count, hipStream_t s) {
+    if (a.n_tasks <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(a.queue, 0, sizeof(int), s);
+    if (e != hipSuccess) return e;
+    if (kp == 64) {
+        constexpr int NG = CFK_PC64_NG, NS = 16 - CFK_PC64_NG;
+        return launch_pc_t<64, NG, NS, 4>(a, cu_count, s);
+    } else if (kp == 128) {
+        return launch_pc_t<128, 4, 4, 2>(a, cu_count, s);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s) {
     if (a.n_tasks <= 0) return hipSuccess;
     const unsigned grid = (unsigned)blocks_for(a.n_tasks);
@@ -2344,13 +2703,8 @@ GenericPlan generic_plan(int precision, int kp) {
 
 template <class T, bool L>
 hipError_t launch_generic_t(const GenericPlan& p, int kp, const SolveArgs& a, hipStream_t s) {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)als_solve_generic<T, L>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_bytes);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    hipError_t e = ensure_dyn_lds((const void*)als_solve_generic<T, L>, (int)p.lds_bytes);
+    if (e != hipSuccess) return e;
     int64_t grid = std::min<int64_t>(a.n_tasks, 4096);
     if (!L) grid = std::min<int64_t>(grid, a.scratch_slabs);
     if (grid <= 0) return hipErrorInvalidValue;

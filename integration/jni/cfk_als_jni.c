@@ -144,7 +144,11 @@ JNIEXPORT void JNICALL Java_de_hpi_collaborativefilteringkafka_nativeals_AlsNati
     }
     jfloat* p = alloc_n(env, n, sizeof(jfloat), "readFactors");
     if (p == NULL) return;
-    if (!fail_status(env, "als_read_factors", als_read_factors(ENGINE(engine), side, row0, n / ld, p, ld)))
+    /* als_read_factors writes the first num_features of each ld-strided row: the rest of the buffer starts as the
+     * Java array's own contents, so the whole-array copy back leaves those columns as they were */
+    (*env)->GetFloatArrayRegion(env, out, 0, n, p);
+    if (!(*env)->ExceptionCheck(env) &&
+        !fail_status(env, "als_read_factors", als_read_factors(ENGINE(engine), side, row0, n / ld, p, ld)))
         (*env)->SetFloatArrayRegion(env, out, 0, n, p);
     free(p);
 }
@@ -177,7 +181,9 @@ JNIEXPORT void JNICALL Java_de_hpi_collaborativefilteringkafka_nativeals_AlsNati
     }
     jdouble* p = alloc_n(env, n, sizeof(jdouble), "readFactorsF64");
     if (p == NULL) return;
-    if (!fail_status(env, "als_read_factors", als_read_factors(ENGINE(engine), side, row0, n / ld, p, ld)))
+    (*env)->GetDoubleArrayRegion(env, out, 0, n, p);   /* untouched columns round-trip (as readFactors) */
+    if (!(*env)->ExceptionCheck(env) &&
+        !fail_status(env, "als_read_factors", als_read_factors(ENGINE(engine), side, row0, n / ld, p, ld)))
         (*env)->SetDoubleArrayRegion(env, out, 0, n, p);
     free(p);
 }

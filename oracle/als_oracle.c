@@ -24,8 +24,8 @@
  *   - f64: the identical algorithm in double with lambda = (double)(float)lambda (ALSAppRunner.java:19
  *          parses lambda with Float.parseFloat). This is the parity oracle (north star: factor max-rel
  *          <= 1e-6, MSE rel <= 1e-6).
- * Known restatement gap: EJML inverts k <= 5 matrices with UnrolledInverseFromMinor_FDRM (cofactors);
- * this oracle uses the LU path for every k. In f64 the two agree to ~1e-15 relative.
+ * CommonOps_FDRM.invert dispatches on the size: k <= UnrolledInverseFromMinor_FDRM.MAX (5) inverts by cofactors
+ * (k = 1: 1/a), larger k by the LU solver above. Both are restated (minor_invert_* below for k <= 5).
  *
  * Also restated:
  *   - the U0 initialiser (UFeatureInitializer.java:50-56): f[0] = (float)mean(ratings) (mean in double),
@@ -142,6 +142,89 @@ DEFINE_LU_INVERT(float, f32, fabsf)
 DEFINE_LU_INVERT(double, f64, fabs)
 
 /* ------------------------------------------------------------------------------------------------ */
+/* EJML UnrolledInverseFromMinor_FDRM / _DDRM restated (CommonOps_FDRM.invert for 2 <= k <= 5)        */
+/* ------------------------------------------------------------------------------------------------ */
+/* inv(mat): scale = 1 / max|a| over all entries (the first entry, then strictly larger ones in storage order),
+ * a_ij *= scale; cofactor m_ij = (-1)^(i+j) det(minor without row i, column j), each minor determinant written
+ * out as the library's generated code does -- Laplace expansion along the minor's first row, terms left to
+ * right with alternating signs (+ a*(..) - b*(..) + ...), 2 x 2 determinants as (a*d - b*c), a negative cofactor
+ * as -( .. ); det = (a11*m11 + a12*m12 + ... + a1k*m1k) / scale; inv[j][i] = m_ij / det. The same expression
+ * shapes evaluated in float (f32, no contraction) or double (f64). */
+#define DEFINE_MINOR_INVERT(T, SUFFIX, ABS)                                                              \
+    static T minor_det_##SUFFIX(const T* a, int n, const int* rows, const int* cols, int m) {            \
+        if (m == 1) return a[rows[0] * n + cols[0]];                                                     \
+        if (m == 2)                                                                                      \
+            return a[rows[0] * n + cols[0]] * a[rows[1] * n + cols[1]] -                                 \
+                   a[rows[0] * n + cols[1]] * a[rows[1] * n + cols[0]];                                  \
+        T total = (T)0;                                                                                  \
+        for (int c = 0; c < m; ++c) {                                                                    \
+            int sub[4], q = 0;                                                                           \
+            for (int x = 0; x < m; ++x)                                                                  \
+                if (x != c) sub[q++] = cols[x];                                                          \
+            const T term = a[rows[0] * n + cols[c]] * minor_det_##SUFFIX(a, n, rows + 1, sub, m - 1);    \
+            total = (c == 0) ? term : ((c & 1) ? total - term : total + term);                           \
+        }                                                                                                \
+        return total;                                                                                    \
+    }                                                                                                    \
+    static void minor_invert_##SUFFIX(T* data, int n) {                                                  \
+        if (n == 1) { data[0] = (T)1 / data[0]; return; }                                                \
+        T max = ABS(data[0]);                                                                            \
+        for (int i = 1; i < n * n; ++i) {                                                                \
+            T v = ABS(data[i]);                                                                          \
+            if (v > max) max = v;                                                                        \
+        }                                                                                                \
+        const T scale = (T)1 / max;                                                                      \
+        T a[25], m[25];                                                                                  \
+        for (int i = 0; i < n * n; ++i) a[i] = data[i] * scale;                                          \
+        for (int i = 0; i < n; ++i)                                                                      \
+            for (int j = 0; j < n; ++j) {                                                                \
+                int rows[4], cols[4], q = 0;                                                             \
+                for (int x = 0; x < n; ++x)                                                              \
+                    if (x != i) rows[q++] = x;                                                           \
+                q = 0;                                                                                   \
+                for (int x = 0; x < n; ++x)                                                              \
+                    if (x != j) cols[q++] = x;                                                           \
+                const T d = minor_det_##SUFFIX(a, n, rows, cols, n - 1);                                 \
+                m[i * n + j] = ((i + j) & 1) ? -(d) : d;                                                 \
+            }                                                                                            \
+        T det = a[0] * m[0];                                                                             \
+        for (int j = 1; j < n; ++j) det = det + a[j] * m[j];                                             \
+        det = det / scale;                                                                               \
+        for (int i = 0; i < n; ++i)                                                                      \
+            for (int j = 0; j < n; ++j) data[j * n + i] = m[i * n + j] / det;                            \
+    }                                                                                                    \
+    /* CommonOps_FDRM.invert(mat): cofactors up to UnrolledInverseFromMinor_FDRM.MAX = 5, else LU */      \
+    static void ejml_invert_##SUFFIX(T* a, int n, T* lu, int* indx, T* col) {                            \
+        if (n <= 5) minor_invert_##SUFFIX(a, n);                                                         \
+        else lu_invert_##SUFFIX(a, n, lu, indx, col);                                                    \
+    }
+
+DEFINE_MINOR_INVERT(float, f32, fabsf)
+DEFINE_MINOR_INVERT(double, f64, fabs)
+
+/* the inverse alone (tests: known-answer matrices through both EJML branches) */
+int oracle_invert_f64(double* a, int n) {
+    if (n < 1 || n > 1024) return 1;
+    double* lu = (double*)malloc(sizeof(double) * ((size_t)n * n + n));
+    int* indx = (int*)malloc(sizeof(int) * (size_t)n);
+    if (!lu || !indx) { free(lu); free(indx); return 2; }
+    ejml_invert_f64(a, n, lu, indx, lu + (size_t)n * n);
+    free(lu);
+    free(indx);
+    return 0;
+}
+int oracle_invert_f32(float* a, int n) {
+    if (n < 1 || n > 1024) return 1;
+    float* lu = (float*)malloc(sizeof(float) * ((size_t)n * n + n));
+    int* indx = (int*)malloc(sizeof(int) * (size_t)n);
+    if (!lu || !indx) { free(lu); free(indx); return 2; }
+    ejml_invert_f32(a, n, lu, indx, lu + (size_t)n * n);
+    free(lu);
+    free(indx);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
 /* The per-entity update (MFeatureCalculator.java:66-104), one CSR row per entity                   */
 /* ------------------------------------------------------------------------------------------------ */
 #define DEFINE_UPDATE(T, SUFFIX)                                                                         \
@@ -170,7 +253,7 @@ DEFINE_LU_INVERT(double, f64, fabs)
         /* A + lambda * ((T)n * I)  (scale(n, identity) then add(A, lambda, N)) */                      \
         T reg = lam * (T)n;                                                                              \
         for (int i = 0; i < k; ++i) A[i * k + i] += reg;                                                 \
-        lu_invert_##SUFFIX(A, k, LU, indx, col);                                                         \
+        ejml_invert_##SUFFIX(A, k, LU, indx, col);                                                       \
         /* m = mult(A^-1, V): total = A[i][0]*V[0]; total += A[i][j]*V[j] */                              \
         for (int i = 0; i < k; ++i) {                                                                    \
             T total = A[i * k] * V[0];                                                                   \

@@ -61,6 +61,10 @@ def lib():
         L.oracle_update_rows_f64.restype = ctypes.c_int
         L.oracle_update_rows_f64.argtypes = [ctypes.c_int64, i64p, i64p, i32p, i16p, f64p, ctypes.c_int,
                                              ctypes.c_float, f64p]
+        L.oracle_invert_f64.restype = ctypes.c_int
+        L.oracle_invert_f64.argtypes = [f64p, ctypes.c_int]
+        L.oracle_invert_f32.restype = ctypes.c_int
+        L.oracle_invert_f32.argtypes = [f32p, ctypes.c_int]
         L.oracle_max_threads.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -181,6 +185,16 @@ def update_side(side: Side, opp: np.ndarray, lam: float, precision: str = "f64",
     rc = fn(n, _p(side.row_ptr, ctypes.c_int64), _p(side.col, ctypes.c_int32), _p(side.ratings, ctypes.c_int16),
             _p(opp, ct), k, float(np.float32(lam)), _p(out, ct), nt)
     assert rc == 0
+    return out
+
+
+def ejml_invert(a: np.ndarray, precision: str = "f64") -> np.ndarray:
+    """CommonOps_FDRM.invert (MFeatureCalculator.java:98) as restated in als_oracle.c: cofactors for k <= 5
+    (UnrolledInverseFromMinor_FDRM), the LU solver beyond."""
+    dt, fn, ct = (np.float64, lib().oracle_invert_f64, ctypes.c_double) if precision == "f64" else \
+        (np.float32, lib().oracle_invert_f32, ctypes.c_float)
+    out = np.ascontiguousarray(a, dt).copy()
+    assert fn(_p(out, ct), out.shape[0]) == 0
     return out
 
 

@@ -339,3 +339,30 @@ def test_device_errors_surface_as_streams_exception(jvm):
         jvm.call("setBlockCoo", h, 0, 1, 0, 4, rows, cols, jvm.array(np.array([5], np.int16)))
     jvm.call("destroy", h)
     assert jvm.stats()["violations"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("f64", [False, True])
+def test_read_factors_with_ld_beyond_k_keeps_padding_columns(jvm, f64):
+    """readFactors[F64] with ld > num_features: columns k..ld-1 of the caller's array keep their values (the shim
+    fills its buffer from the Java array before als_read_factors, which writes only the first k per row), as the
+    Panama binding (AlsFfm.readFactors) leaves them."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    k, ld, n = 3, 5, 4
+    dt = np.float64 if f64 else np.float32
+    h = jvm.call("create", 0, k, 1 if f64 else 0)
+    try:
+        jvm.call("allocFactors", h, 0, n)
+        src = (np.arange(n * k, dtype=dt) + 1.0) / 7.0
+        jvm.call("writeFactorsF64" if f64 else "writeFactors", h, 0, 0, jvm.array(src), k)
+        init = np.full(n * ld, -7.25, dt)
+        out = jvm.array(init)
+        jvm.call("readFactorsF64" if f64 else "readFactors", h, 0, 0, out, ld)
+        got = jvm.read(out, dt).reshape(n, ld)
+        assert np.array_equal(got[:, :k], src.reshape(n, k))
+        assert np.all(got[:, k:] == -7.25)
+    finally:
+        jvm.call("destroy", h)
+    assert jvm.stats()["violations"] == 0

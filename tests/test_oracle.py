@@ -110,3 +110,42 @@ def test_java_double_format(oracle_mod):
     assert f(float(np.float32(3.52))) == "3.5199999809265137"
     assert f(1.0) == "1.0" and f(100.0) == "100.0" and f(0.001) == "0.001"
     assert f(1e-5) == "1.0E-5" and f(1e7) == "1.0E7" and f(-2.5e-10) == "-2.5E-10" and f(0.0) == "0.0"
+
+
+def test_ejml_invert_branches(oracle_mod):
+    """CommonOps_FDRM.invert (MFeatureCalculator.java:98): UnrolledInverseFromMinor_FDRM for k <= 5, LU beyond.
+    Both restated branches invert regularised Gram systems to f64 round-off, and the k = 2, 3 cofactor forms equal,
+    bit for bit in float, the library's inv2 / inv3 expressions (scale by 1/max|a|, cofactors, det over scale)."""
+    rng = np.random.default_rng(11)
+    for k in range(1, 9):
+        Y = rng.random((3 * k + 2, k))
+        A = Y.T @ Y + 0.05 * len(Y) * np.eye(k)
+        inv = oracle_mod.ejml_invert(A, "f64")
+        assert np.abs(inv - np.linalg.inv(A)).max() <= 1e-12 * np.abs(np.linalg.inv(A)).max(), k
+        inv32 = oracle_mod.ejml_invert(A.astype(np.float32), "f32")
+        assert np.abs(inv32 - np.linalg.inv(A)).max() <= 1e-4 * np.abs(np.linalg.inv(A)).max(), k
+    f = np.float32
+    for k in (2, 3):
+        Y = rng.random((7, k)).astype(f)
+        A = (Y.T @ Y + f(0.35) * np.eye(k, dtype=f)).astype(f)
+        mx = np.abs(A).max()
+        sc = f(1) / mx
+        a = A * sc
+        if k == 2:
+            m = np.array([[a[1, 1], -a[1, 0]], [-a[0, 1], a[0, 0]]], f)
+            det = (a[0, 0] * m[0, 0] + a[0, 1] * m[0, 1]) / sc
+        else:
+            m = np.empty((3, 3), f)
+            m[0, 0] = a[1, 1] * a[2, 2] - a[1, 2] * a[2, 1]
+            m[0, 1] = -(a[1, 0] * a[2, 2] - a[1, 2] * a[2, 0])
+            m[0, 2] = a[1, 0] * a[2, 1] - a[1, 1] * a[2, 0]
+            m[1, 0] = -(a[0, 1] * a[2, 2] - a[0, 2] * a[2, 1])
+            m[1, 1] = a[0, 0] * a[2, 2] - a[0, 2] * a[2, 0]
+            m[1, 2] = -(a[0, 0] * a[2, 1] - a[0, 1] * a[2, 0])
+            m[2, 0] = a[0, 1] * a[1, 2] - a[0, 2] * a[1, 1]
+            m[2, 1] = -(a[0, 0] * a[1, 2] - a[0, 2] * a[1, 0])
+            m[2, 2] = a[0, 0] * a[1, 1] - a[0, 1] * a[1, 0]
+            det = ((a[0, 0] * m[0, 0] + a[0, 1] * m[0, 1]) + a[0, 2] * m[0, 2]) / sc
+        want = (m / det).T.astype(f)
+        got = oracle_mod.ejml_invert(A, "f32")
+        assert np.array_equal(got, want), (k, got, want)

@@ -6,7 +6,8 @@
       --variants "ALS_DEBUG_SKIP_SOLVE=0" "ALS_DEBUG_SKIP_SOLVE=1"   # Gram / solve split: debug build only
 
 Each variant is a set of env settings read at engine creation / block upload. Prints per-variant median and
-min device time (HIP events) of the main + reduce launches of each half on the Netflix-shape workload.
+min device time (HIP events) of the main + reduce launches of each half on the Netflix-shape workload. Every
+timed half starts from the same snapshot of real factor tables (two iterations from the seeded U0).
 """
 from __future__ import annotations
 
@@ -37,12 +38,14 @@ def main():
     ds = cfk.Dataset.synthetic_netflix(args.users, args.movies, args.nnz, 0xA15, nthreads=16)
     blocks = [ds.shard_block(0), ds.shard_block(1)]
     kp = cfk.factor_stride(args.k)
-    U = torch.zeros((blocks[1]["n_slots"] + 1, kp), dtype=torch.float32, device="cuda")
-    M = torch.zeros((blocks[0]["n_slots"] + 1, kp), dtype=torch.float32, device="cuda")
-    engines = []
-    for v in args.variants:
+
+    def tables():
+        return (torch.zeros((blocks[0]["n_slots"] + 1, kp), dtype=torch.float32, device="cuda"),
+                torch.zeros((blocks[1]["n_slots"] + 1, kp), dtype=torch.float32, device="cuda"))
+
+    def make_engine(env, M, U):
         saved = dict(os.environ)
-        for kv in v.split(","):
+        for kv in env.split(","):
             if kv:
                 k, val = kv.split("=")
                 os.environ[k] = val
@@ -55,32 +58,69 @@ def main():
             eng.set_block(side, b["row_ptr"], b["col"], b["ratings"], 0, blocks[1 - side]["n_slots"])
         os.environ.clear()
         os.environ.update(saved)
-        engines.append(eng)
-    engines[0].write_factors(1, ds.init_user_factors(args.k, 42))
-    for e in engines:        # warm up every variant
-        e.solve_half(0, 0.05)
-        e.solve_half(1, 0.05)
+        return eng
+
+    # Canonical input state: two real iterations from the seeded U0 on a plain engine. Every timed half of every
+    # variant starts from this snapshot in the variant's own tables, so a work-dropping variant (debug SKIP_SOLVE)
+    # never feeds its garbage to another half, and every variant's MFMAs see the same data (MFMA power, and
+    # so the clock, depends on the operand values).
+    Ms, Us = tables()
+    ref = make_engine("", Ms, Us)
+    ref.write_factors(1, ds.init_user_factors(args.k, 42))
+    for _ in range(2):
+        ref.solve_half(0, 0.05)
+        ref.solve_half(1, 0.05)
     torch.cuda.synchronize()
+    del ref
+    engines = []
+    for v in args.variants:
+        M, U = tables()
+        engines.append((make_engine(v, M, U), M, U))
     res = {v: {"movie": [], "user": [], "movie_reduce": [], "user_reduce": []} for v in args.variants}
-    for r in range(args.rounds):
-        for v, e in zip(args.variants, engines):
+    for r in range(args.rounds + 1):   # round 0: warm-up
+        for v, (e, M, U) in zip(args.variants, engines):
             e.set_timing(True)
-            e.solve_half(0, 0.05)
-            e.solve_half(1, 0.05)
+            for side in (0, 1):
+                M.copy_(Ms)
+                U.copy_(Us)
+                e.solve_half(side, 0.05)
             torch.cuda.synchronize()
             gm, rm, _ = e.timing_collect(0)
             gu, ru, _ = e.timing_collect(1)
             e.set_timing(False)
+            if r == 0:
+                continue
             res[v]["movie"].append(gm)
             res[v]["user"].append(gu)
             res[v]["movie_reduce"].append(rm)
             res[v]["user_reduce"].append(ru)
+    # results of each variant's halves (both from the snapshot) against the first variant's
+    outs = []
+    for v, (e, M, U) in zip(args.variants, engines):
+        res_v = []
+        for side in (0, 1):
+            M.copy_(Ms)
+            U.copy_(Us)
+            e.solve_half(side, 0.05)
+            torch.cuda.synchronize()
+            res_v.append((M if side == 0 else U).clone())
+        outs.append(res_v)
+    diffs = {}
+    for v, r in zip(args.variants, outs):
+        d = {}
+        for side, name in ((0, "movie"), (1, "user")):
+            ref_t, t = outs[0][side], r[side]
+            d[name] = {"bitwise_equal": bool(torch.equal(ref_t, t)),
+                       "max_abs_over_max": float((t - ref_t).abs().max() / ref_t.abs().max().clamp_min(1e-30)),
+                       "finite": bool(torch.isfinite(t).all())}
+        diffs[v] = d
+        print("vs", args.variants[0], ":", v, json.dumps(d), flush=True)
     out = {}
     for v in args.variants:
         out[v] = {k: {"median_ms": statistics.median(x), "min_ms": min(x)} for k, x in res[v].items()}
         out[v]["total_median_ms"] = sum(out[v][k]["median_ms"] for k in ("movie", "user", "movie_reduce", "user_reduce"))
         print(v, json.dumps(out[v]), flush=True)
-    print(json.dumps({"kbench": out, "nnz": args.nnz, "k": args.k}))
+    print(json.dumps({"kbench": out, "nnz": args.nnz, "k": args.k, "diffs": diffs}))
 
 
 if __name__ == "__main__":
