@@ -2,7 +2,7 @@
 """bench.py -- ALS ratings/sec per full iteration, Netflix-shape k=64 fp32 on 1..8 MI355X (BASELINE.json).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload netflix|powerlaw] [--k 64|128]
-                  [--exchange torch|native]
+                  [--exchange native|torch] [--movie-chunks C]
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
       bench.py --gpus N --steps K --warmup W
 
@@ -45,6 +45,7 @@ MFMA16_PEAK_TFS = 2500.0     # dense bf16 / f16 MFMA peak (no sparsity; the f16 
 IC_GATHER_CEILING_GBS = 7900.0
 L2_GATHER_CEILING_GBS = 18800.0
 L2_RESIDENT_BYTES = 8 << 20  # a gathered table this small stays in every XCD's 4 MiB L2 to most of its rows
+IC_RESIDENT_BYTES = 256 << 20   # Infinity Cache: a larger gathered table streams from HBM (configs[4]'s 2.56 GB U)
 MFMA_FLOP = 16 * 16 * 32 * 2   # one v_mfma_f32_16x16x32_{bf16,f16}
 WORKLOADS = {"netflix": (480_189, 17_770, 100_000_000), "powerlaw": (10_000_000, 1_000_000, 2_000_000_000)}
 
@@ -202,10 +203,18 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=7.0, help="CPU baseline seconds per thread count")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--overlap-chunks", type=int, default=4, help="user-half chunks per all-gather overlap (N > 1)")
-    ap.add_argument("--exchange", choices=("torch", "native"), default="torch",
-                    help="N > 1: all-gathers through torch.distributed (RCCL) or through the engine's own RCCL "
-                         "communicator behind the C ABI (als_comm_init / als_allgather_shard, the path a JNI caller "
-                         "binds)")
+    ap.add_argument("--exchange", choices=("torch", "native"), default="native",
+                    help="N > 1: all-gathers through the engine's own RCCL communicator behind the C ABI (default: "
+                         "als_comm_init / als_allgather_shard, the path a JNI caller binds) or through "
+                         "torch.distributed (RCCL); the one-GPU gloo rehearsal always uses torch")
+    ap.add_argument("--movie-chunks", type=int, default=None,
+                    help="N > 1: movie-half exchange chunks (default: --overlap-chunks once the movie table exceeds "
+                         "8 MB, e.g. configs[4]; else 1)")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="G > 1: run ONE rank's work of a G-GPU job on this GPU (shard --shard-rank of G, synthesized "
+                         "alone, no exchange): the per-GPU compute of a sharded config such as configs[4] on 8 GPUs; "
+                         "value = that rank's ratings per second")
+    ap.add_argument("--shard-rank", type=int, default=0)
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N > 1 ranks all on cuda:0 over gloo: rehearses the multi-rank driver on a one-GPU box "
                          "(RCCL needs one GPU per rank); not a performance configuration")
@@ -214,18 +223,20 @@ def main():
     users, movies = args.users or users, args.movies or movies
     nnz_total = args.nnz or nnz_total
 
-    lib_env = os.environ.get("CFK_ALS_LIB", "")
-    if "build_debug" in lib_env:
-        sys.exit(f"bench: CFK_ALS_LIB={lib_env} is the diagnostics build (work-dropping knobs): refused")
-
     import torch
     import torch.distributed as dist
     import __graft_entry__
     cfk = __graft_entry__.load_package()
+    from cfk_amd import _lib
+    if hasattr(_lib.lib(), "als_debug_knobs_compiled"):   # exported by the diagnostics build only, whatever its path
+        sys.exit(f"bench: {_lib.LIB_PATH} is the diagnostics build (work-dropping knobs compiled in): refused")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    solo = args.shard_of > 1   # one rank of a G-GPU job, alone on this GPU
+    if solo and world > 1:
+        sys.exit("bench: --shard-of runs one process")
     if world != args.gpus and rank == 0:
         print(f"bench: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
     if args.rehearse_one_gpu:
@@ -243,21 +254,26 @@ def main():
 
     t_setup = time.perf_counter()
     nthreads = min(16, os.cpu_count() or 1)
-    if world > 1:   # this rank's ratings only (both sides' in-blocks of shard `rank`)
+    if solo:
+        ds = cfk.Dataset.synthetic_shard(args.workload, users, movies, nnz_total, args.seed, args.shard_of,
+                                         args.shard_rank, nthreads)
+    elif world > 1:   # this rank's ratings only (both sides' in-blocks of shard `rank`)
         ds = cfk.Dataset.synthetic_shard(args.workload, users, movies, nnz_total, args.seed, world, rank, nthreads)
     elif args.workload == "powerlaw":
         ds = cfk.Dataset.synthetic_powerlaw(users, movies, nnz_total, args.seed, nthreads=nthreads)
     else:
         ds = cfk.Dataset.synthetic_netflix(users, movies, nnz_total, args.seed, nthreads=nthreads)
     nm, nu, nnz_local = ds.counts()
-    exchange = args.exchange if world > 1 and not args.rehearse_one_gpu else "torch"
-    app = cfk.ALSApp(world, args.k, args.lam, args.steps, precision="f32", seed=42, device=local, rank=rank,
-                     world_size=world, overlap_chunks=args.overlap_chunks,
-                     exchange=exchange).setup(ds, check_duplicates=False)
+    exchange = "none" if solo else args.exchange if world > 1 and not args.rehearse_one_gpu else "torch"
+    gsim, rsim = (args.shard_of, args.shard_rank) if solo else (world, rank)
+    app = cfk.ALSApp(gsim, args.k, args.lam, args.steps, precision="f32", seed=42, device=local, rank=rsim,
+                     world_size=gsim, overlap_chunks=args.overlap_chunks, exchange=exchange,
+                     movie_chunks=args.movie_chunks).setup(ds, check_duplicates=False)
     t_setup = time.perf_counter() - t_setup
     # ranks the exchange spans: the engine's own communicator (native) or the torch process group; RCCL unless the
     # one-GPU rehearsal runs the group over gloo
-    exchange_world = app.engine.comm_info()[0] if exchange == "native" else (dist.get_world_size() if world > 1 else 1)
+    exchange_world = (app.engine.comm_info()[0] if exchange == "native" else
+                      dist.get_world_size() if world > 1 else 1)
     rccl_world = None if args.rehearse_one_gpu else exchange_world
 
     for _ in range(args.warmup):
@@ -287,7 +303,7 @@ def main():
     for side in ("movie", "user"):
         g, r, _ = eng.timing_collect(side)
         g_ms[side], r_ms[side] = g / K, r / K
-    mse = app.mse()
+    mse = app.mse() if not solo else None   # a lone shard's factors are not a model
 
     if rank == 0:
         build = build_record()
@@ -317,13 +333,18 @@ def main():
                         + 4 * kp * i["n_rows"])
             opp_rows = info["user" if side == "movie" else "movie"]["n_slots"] + 1
             table_bytes = opp_rows * 4 * kp
-            gceil = L2_GATHER_CEILING_GBS if table_bytes <= L2_RESIDENT_BYTES else IC_GATHER_CEILING_GBS
+            # where the gathered rows are served from: the XCD's L2, the Infinity Cache, or (beyond it) HBM
+            where = "l2" if table_bytes <= L2_RESIDENT_BYTES else "ic" if table_bytes <= IC_RESIDENT_BYTES else "hbm"
+            gceil = {"l2": L2_GATHER_CEILING_GBS, "ic": IC_GATHER_CEILING_GBS, "hbm": HBM_PEAK_GBS}[where]
             mfma_frac = mf / t_s / 1e12 / MFMA16_PEAK_TFS if mf else 0.0
             # rows of a table beyond the L2 are served by the Infinity Cache: measure them with the fabric-side counter
             # bytes of this build (L2 hits excluded) when profiled, else with the bytes requested (then an upper
             # bound that can exceed the ceiling by the L2 hit share)
             fab = c.get("hbm_bytes") if c else None
-            g_bytes = fab if (fab and gceil == IC_GATHER_CEILING_GBS) else gathered
+            if where == "hbm":   # the §8d roofline binds: algorithmic bytes against HBM peak
+                g_bytes = b
+            else:
+                g_bytes = fab if (fab and where == "ic") else gathered
             gather_frac = g_bytes / t_s / 1e9 / gceil
             d = {
                 # <KP, waves per SIMD, ...>: the instantiations launch_solve picks (als_kernels.hip, CFK_PS64_WAVES)
@@ -334,11 +355,12 @@ def main():
                 "mfma": {"per_32_entry_block": mfma_per_block(kp, path["presplit"]), "flop_per_launch": mf,
                          "executed_tflops": mf / t_s / 1e12, "peak": MFMA16_PEAK_TFS, "frac": mfma_frac},
                 "gather": {"bytes_requested": gathered, "bytes": g_bytes,
-                           "bytes_source": "PMC FETCH_SIZE x2 + WRITE_SIZE" if g_bytes is not gathered else "requested",
-                           "opposite_table_bytes": table_bytes, "achieved_gbs": g_bytes / t_s / 1e9,
-                           "ceiling_gbs": gceil, "frac": gather_frac,
-                           "ceiling": "L2-resident rows" if gceil == L2_GATHER_CEILING_GBS else
-                                      "Infinity-Cache random rows"},
+                           "bytes_source": ("SURVEY.md §8d algorithmic bytes" if where == "hbm" else
+                                            "PMC FETCH_SIZE x2 + WRITE_SIZE" if g_bytes is not gathered else "requested"),
+                           "opposite_table_bytes": table_bytes, "served_from": where,
+                           "achieved_gbs": g_bytes / t_s / 1e9, "ceiling_gbs": gceil, "frac": gather_frac,
+                           "ceiling": {"l2": "L2-resident rows", "ic": "Infinity-Cache random rows",
+                                       "hbm": "HBM peak (table beyond the Infinity Cache)"}[where]},
                 "algorithmic_bytes": {"bytes": b, "achieved_gbs": b / t_s / 1e9, "frac_of_hbm": b / t_s / 1e9 / HBM_PEAK_GBS,
                                       "note": "SURVEY.md §8d algorithmic bytes / launch time; cache-served gathers "
                                               "included, so it can exceed 1: not a bound"},
@@ -356,15 +378,20 @@ def main():
                 d.update(bound="mfma", unit="TFLOP/s", peak=MFMA16_PEAK_TFS, achieved=mf / t_s / 1e12, frac=mfma_frac,
                          limit="MFMA pipe: the Gram's 16x16x32 MFMA flops as issued (whole launch, solve phase "
                                "included) against the dense bf16/f16 peak")
+            elif where == "hbm":
+                d.update(bound="hbm", unit="GB/s", peak=gceil, achieved=g_bytes / t_s / 1e9, frac=gather_frac,
+                         limit="HBM: SURVEY.md §8d algorithmic bytes per launch / launch time against the 8 TB/s HBM "
+                               "peak (the gathered table exceeds the 256 MiB Infinity Cache)")
             else:
-                d.update(bound="gather", unit="GB/s", peak=gceil, achieved=g_bytes / t_s / 1e9, frac=gather_frac,
+                d.update(bound=f"{where}_gather", unit="GB/s", peak=gceil, achieved=g_bytes / t_s / 1e9,
+                         frac=gather_frac,
                          limit="gather of the opposite factor rows: bytes requested per launch / launch time against "
                                f"the chip's {d['gather']['ceiling']} gather ceiling (MI355X_MICROARCH.md)")
             per[side] = d
         dom = max(per, key=lambda s: per[s]["avg_launch_ms"])
         d = per[dom]
         roofline = {
-            "bound": "mfma" if d["bound"] == "mfma" else "hbm", "limiter": d["bound"],
+            "bound": d["bound"], "limiter": d["bound"],
             "achieved": d["achieved"], "peak": d["peak"],
             "unit": d["unit"], "frac": d["frac"], "traffic": d.get("traffic"),
             "kernel": d["kernel"] + f" ({dom} half, the dominant launch)", "limit": d["limit"],
@@ -377,18 +404,21 @@ def main():
                                            / ((g_ms["movie"] + g_ms["user"]) / 1000.0) / 1e9,
             "per_launch": per,
             "counters_source": (ctr or {}).get("source"),
-            "note": "achieved/frac: the dominant launch against the ceiling it is closest to (limiter; bound = its "
-                    "memory (hbm) or compute (mfma) side): executed 16x16x32 MFMA flops against the dense bf16/f16 "
-                    "peak, or the gathered bytes it requests / launch time against the chip's gather ceiling for "
-                    "where those rows are served from (MI355X_MICROARCH.md); traffic = PMC FETCH_SIZE x2 + WRITE_SIZE "
-                    "per launch; counters = rocprofv3 SQ passes of this build",
+            "note": "achieved/frac: the dominant launch against the ceiling it is closest to (bound: mfma = "
+                    "executed 16x16x32 MFMA flops against the dense bf16/f16 peak; l2_gather / ic_gather = the "
+                    "gathered bytes it requests / launch time against the chip's gather ceiling for rows served from "
+                    "the L2 / the Infinity Cache (MI355X_MICROARCH.md); hbm = SURVEY.md §8d algorithmic bytes against "
+                    "the HBM peak when the gathered table exceeds the Infinity Cache); traffic = PMC FETCH_SIZE x2 + "
+                    "WRITE_SIZE per launch; counters = rocprofv3 SQ passes of this build",
         }
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not solo and not args.no_cpu_baseline:
             share, share_src = cpu_share()
             counts = [4] + ([share] if share != 4 else [])      # reference's stream threads, the box's share
             cpu = cpu_baseline(ds, args.k, args.lam, args.cpu_seconds, counts, share_src)
-        value = nnz_total * K / elapsed
+        # whole-job ratings per second; --shard-of: this rank's share (its in-block entries, averaged over the halves)
+        shard_nnz = (info["movie"]["nnz"] + info["user"]["nnz"]) / 2
+        value = (shard_nnz if solo else nnz_total) * K / elapsed
         wl = (f"{args.workload}-shape synthetic {nu} users x {nm} movies x {nnz_total} ratings, k={args.k}, "
               f"lambda={args.lam}, one step = one full ALS iteration")
         line = {
@@ -403,8 +433,12 @@ def main():
                        "exchange": exchange if world > 1 else None, "rccl_world": rccl_world,
                        "exchange_world": exchange_world,
                        "overlap_chunks": args.overlap_chunks if world > 1 else None,
-                       "rehearsal_gloo_one_gpu": bool(args.rehearse_one_gpu)},
-            "solves_per_s": (nm + nu) * K / elapsed,
+                       "movie_chunks": app.info[0]["n_chunks"] if world > 1 else None,
+                       "rehearsal_gloo_one_gpu": bool(args.rehearse_one_gpu),
+                       "shard_of": args.shard_of if solo else None, "shard_rank": args.shard_rank if solo else None,
+                       "shard_ratings": shard_nnz if solo else None},
+            "solves_per_s": ((info["movie"]["n_rows"] + info["user"]["n_rows"]) if solo else (nm + nu)) * K / elapsed,
+            "projected_job_ratings_per_s_compute_only": value * args.shard_of if solo else None,
             "mse_after": mse,
             "setup_s": t_setup,
             "build": build,

@@ -25,10 +25,12 @@ from .engine import ALSEngine, Dataset, SIDE_MOVIE, SIDE_USER
 
 
 class ALSApp:
+    MOVIE_CHUNK_BYTES = 8 << 20   # a movie factor table above this is exchanged in chunks (N > 1)
+
     def __init__(self, num_partitions: int, num_features: int, als_lambda: float, num_als_iterations: int,
                  num_movies: int | None = None, num_users: int | None = None, *, precision: str = "f32",
                  seed: int = 42, device: int = 0, rank: int = 0, world_size: int = 1, group=None,
-                 overlap_chunks: int = 4, exchange: str = "torch"):
+                 overlap_chunks: int = 4, exchange: str = "torch", movie_chunks: int | None = None):
         self.NUM_PARTITIONS = num_partitions
         self.NUM_FEATURES = num_features
         self.ALS_LAMBDA = float(np.float32(als_lambda))     # Float.parseFloat (ALSAppRunner.java:19)
@@ -47,12 +49,16 @@ class ALSApp:
         # user half on > 1 GPU: solve in `overlap_chunks` row ranges and all-gather each range while the
         # next one is solved (1 = one launch, then one all-gather)
         self.overlap_chunks = max(1, int(overlap_chunks))
-        self.chunk_slots = None
+        # movie half on > 1 GPU: the same chunked exchange once the movie table is large (None: overlap_chunks
+        # chunks when the movie factor table exceeds MOVIE_CHUNK_BYTES, e.g. configs[4]'s 1M items; 1 = unchunked)
+        self.movie_chunks = None if movie_chunks is None else max(1, int(movie_chunks))
+        self.chunk_slots = [None, None]   # per side: chunk indices of a chunked half, or None
         # "torch": torch.distributed collectives on the factor tensors (backend "nccl" = RCCL); "native": the
         # engine's own RCCL communicator through the C ABI (als_comm_init / als_allgather_shard), the path a
         # JNI caller uses. The rendezvous (sharing the RCCL unique id) uses the torch process group either way.
-        if exchange not in ("torch", "native"):
-            raise ValueError("exchange must be 'torch' or 'native'")
+        # "none": no exchange at all -- one rank of a sharded run timed alone (its halves, not the all-gathers).
+        if exchange not in ("torch", "native", "none"):
+            raise ValueError("exchange must be 'torch', 'native' or 'none'")
         self.exchange = exchange
 
     # -------------------------------------------------------------------------------------------------
@@ -73,10 +79,17 @@ class ALSApp:
                              "(MFeatureCalculator.java:65)")
         self.ds = ds
         # user half on > 1 GPU in `overlap_chunks` row ranges: chunk-major user slots (include/als_host.h "Slot
-        # layout"), so each range's exchange is one contiguous all-gather
-        n_chunks = self.overlap_chunks if self.world > 1 else 1
-        ds.set_slot_chunks(SIDE_USER, n_chunks)
-        ds.set_slot_chunks(SIDE_MOVIE, 1)
+        # layout"), so each range's exchange is one contiguous all-gather; the movie half too once its table is big
+        kp = (self.NUM_FEATURES + 15) // 16 * 16
+        if self.world == 1:
+            n_chunks = [1, 1]
+        else:
+            mc = self.movie_chunks
+            if mc is None:
+                mc = self.overlap_chunks if nm * kp * 4 > self.MOVIE_CHUNK_BYTES else 1
+            n_chunks = [mc, self.overlap_chunks]
+        ds.set_slot_chunks(SIDE_USER, n_chunks[SIDE_USER])
+        ds.set_slot_chunks(SIDE_MOVIE, n_chunks[SIDE_MOVIE])
         if engine_factory is None:
             torch.cuda.set_device(self.device)
             eng = ALSEngine(self.NUM_FEATURES, self.precision, self.device)
@@ -101,11 +114,13 @@ class ALSApp:
                 eng.set_row_layout(side, sc, self.world * sc)
             self.info[side] = {k: blk[k] for k in ("n_rows", "row_offset", "nnz", "slots_per_shard", "n_slots",
                                                    "slots_per_chunk", "n_chunks")}
-        if n_chunks > 1:
-            sc, n = self.info[SIDE_USER]["slots_per_chunk"], self.info[SIDE_USER]["n_rows"]
-            # chunk c = this rank's local rows [c Sc, (c+1) Sc) = factor rows [c G Sc + rank Sc, + Sc)
-            self.chunk_slots = list(range(n_chunks))
-            eng.set_chunks(SIDE_USER, [min(c * sc, n) for c in range(n_chunks)] + [n])
+        for side in (SIDE_MOVIE, SIDE_USER):
+            nc = self.info[side]["n_chunks"]
+            if nc > 1:
+                sc, n = self.info[side]["slots_per_chunk"], self.info[side]["n_rows"]
+                # chunk c = this rank's local rows [c Sc, (c+1) Sc) = factor rows [c G Sc + rank Sc, + Sc)
+                self.chunk_slots[side] = list(range(nc))
+                eng.set_chunks(side, [min(c * sc, n) for c in range(nc)] + [n])
         u0 = ds.init_user_factors(self.NUM_FEATURES, self.seed, self.world)
         eng.write_factors(SIDE_USER, u0)
         if self.exchange == "native" and self.world > 1:
@@ -129,7 +144,7 @@ class ALSApp:
     def _allgather(self, side: int, chunk: int = 0):
         """Exchange chunk `chunk` of `side` (the whole shard when the side is unchunked): one all-gather of the G
         ranks' Sc-row pieces, which are contiguous in the chunk-major slot layout."""
-        if self.world == 1:
+        if self.world == 1 or self.exchange == "none":   # "none": one rank's work alone (bench.py --shard-of)
             return
         sc = self.info[side]["slots_per_chunk"]
         if self.exchange == "native":
@@ -144,29 +159,29 @@ class ALSApp:
                                            full[base + self.rank * sc:base + (self.rank + 1) * sc],
                                            group=self.group, async_op=True)
 
-    def movie_half(self):
-        """MFeatureCalculator-i over this rank's movies + all-gather (movie-features-i topic)."""
-        self.engine.solve_half(SIDE_MOVIE, self.ALS_LAMBDA)
-        w = self._allgather(SIDE_MOVIE)
-        if w is not None:
-            w.wait()
-
-    def user_half(self):
-        """UFeatureCalculator-i over this rank's users + all-gather (user-features-(i+1) topic)."""
-        if self.chunk_slots is None:
-            self.engine.solve_half(SIDE_USER, self.ALS_LAMBDA)
-            w = self._allgather(SIDE_USER)
+    def _half(self, side):
+        if self.chunk_slots[side] is None:
+            self.engine.solve_half(side, self.ALS_LAMBDA)
+            w = self._allgather(side)
             if w is not None:
                 w.wait()
             return
         # chunk c's all-gather (RCCL, ordered after chunk c's solve on the stream) overlaps chunk c+1's solve
         works = []
-        for c in self.chunk_slots:
-            self.engine.solve_half_chunk(SIDE_USER, self.ALS_LAMBDA, c)
-            works.append(self._allgather(SIDE_USER, c))
+        for c in self.chunk_slots[side]:
+            self.engine.solve_half_chunk(side, self.ALS_LAMBDA, c)
+            works.append(self._allgather(side, c))
         for w in works:
             if w is not None:
                 w.wait()
+
+    def movie_half(self):
+        """MFeatureCalculator-i over this rank's movies + all-gather (movie-features-i topic)."""
+        self._half(SIDE_MOVIE)
+
+    def user_half(self):
+        """UFeatureCalculator-i over this rank's users + all-gather (user-features-(i+1) topic)."""
+        self._half(SIDE_USER)
 
     def iteration(self):
         self.movie_half()

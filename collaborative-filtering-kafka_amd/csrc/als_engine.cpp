@@ -64,6 +64,7 @@ struct Block {
     Task* d_sq_tasks = nullptr;     // every FULL + PARTIAL task incl. the short rows (als_sq_error)
     int32_t n_sq = 0;
     bool presplit = false;          // gather a pre-split (scaled fp16 h/m) copy of the opposite table
+    bool rat_exact16 = false;       // every rating of the block is an integer |r| <= 2048 (exact in fp16)
     // chunk-major slot layout (als_set_row_layout): local row i -> factor row row_offset + (i / rows_per_chunk) *
     // chunk_stride + i % rows_per_chunk; rows_per_chunk = 0: row_offset + i
     int64_t rows_per_chunk = 0, chunk_stride = 0;
@@ -109,6 +110,7 @@ struct als_engine {
     size_t stage_bytes = 0;
     uint32_t* d_integrity = nullptr;   // cfk::INTEGRITY_WORDS: partial slots that failed their check
     int* d_queue = nullptr;         // task counter of the pipelined pre-split launch (cfk::launch_solve_pc)
+    unsigned long long* d_pc_stats = nullptr;   // debug build: cycle accounting of the pipelined launch
     int cu_count = 0;               // compute units of the device: the pipelined launch's grid
     // pre-split halves through the pipelined launch (Gram waves hand systems to solver waves, cfk::launch_solve_pc)
     // with ALS_PC=1; default: the one-kernel launch (each wave Gram then solve)
@@ -282,6 +284,9 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
     if (const char* env = getenv("ALS_DEBUG_REDUCE_GEN_SKEW")) e->debug_gen_skew = (uint32_t)atoi(env);
     if (const char* env = getenv("ALS_DEBUG_FIXED_GEN")) e->debug_fixed_gen = env[0] == '1';
     if (const char* env = getenv("ALS_DEBUG_EXTRA_LDS")) e->debug_extra_lds = atoi(env);
+    if (hipMalloc((void**)&e->d_pc_stats, cfk::PC_STAT_N * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(e->d_pc_stats, 0, cfk::PC_STAT_N * sizeof(unsigned long long)) != hipSuccess)
+        e->d_pc_stats = nullptr;
 #endif
     if (const char* env = getenv("ALS_REFINE_MIN_PIVOT")) {
         // the product library can only refine MORE often than the validated gate (> 1: every row); thresholds
@@ -300,10 +305,10 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
     }
     e->own_stream = true;
     st = hipDeviceGetAttribute(&e->cu_count, hipDeviceAttributeMultiprocessorCount, device);
-    if (st == hipSuccess) st = hipMalloc((void**)&e->d_queue, sizeof(int));
+    if (st == hipSuccess) st = hipMalloc((void**)&e->d_queue, cfk::PC_QUEUE_INTS * sizeof(int));
     if (st == hipSuccess) st = hipMalloc((void**)&e->d_integrity, cfk::INTEGRITY_WORDS * sizeof(uint32_t));
     if (st == hipSuccess) st = hipMemset(e->d_integrity, 0, cfk::INTEGRITY_WORDS * sizeof(uint32_t));
-    if (st == hipSuccess) st = hipMalloc((void**)&e->d_amax, sizeof(uint32_t));
+    if (st == hipSuccess) st = hipMalloc((void**)&e->d_amax, 2 * sizeof(uint32_t));
     if (st != hipSuccess) {
         (void)hipStreamDestroy(e->stream);
         (void)hipFree(e->d_integrity);
@@ -328,6 +333,7 @@ int als_engine_destroy(als_engine* e) {
     (void)hipHostFree(e->h_stage);
     (void)hipFree(e->d_integrity);
     (void)hipFree(e->d_queue);
+    (void)hipFree(e->d_pc_stats);
     (void)hipFree(e->d_amax);
     for (auto& rec : e->pending)
         for (auto ev : rec.ev) (void)hipEventDestroy(ev);
@@ -405,13 +411,20 @@ int check_block_shape(als_engine* e, int64_t n_rows, int64_t row_offset, int64_t
 }
 
 // Padded entries of a row of degree d (every row starts on a 32-entry block).
+// every rating r satisfies |r| <= 2048, so rh = fp16(r) = r and rm = 0 (the pre-split RHS can skip the rm pairs)
+bool ratings_exact16(const int16_t* r, int64_t n) {
+    for (int64_t i = 0; i < n; ++i)
+        if (r[i] > 2048 || r[i] < -2048) return false;
+    return true;
+}
 inline int64_t padded(int64_t d) { return (d + cfk::BLOCK_ENTRIES - 1) / cfk::BLOCK_ENTRIES * cfk::BLOCK_ENTRIES; }
 
 // Work plan of a block whose padded in-block (d_col / d_rat, device, already laid out) has row degrees deg[]
 // and row starts begin[]: FULL / PARTIAL / REDUCE tasks, longest first; uploads the plan, takes ownership of
 // d_col / d_rat and sizes the partial and pre-split workspaces.
 int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows, int64_t nnz,
-                 const std::vector<int64_t>& deg, const std::vector<int64_t>& begin, int32_t* d_col, float* d_rat) {
+                 const std::vector<int64_t>& deg, const std::vector<int64_t>& begin, int32_t* d_col, float* d_rat,
+                 bool rat_exact16) {
     const int64_t nnz_padded = begin[n_rows];
     auto drop = [&]() {
         (void)hipFree(d_col);
@@ -481,8 +494,23 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     }
     // Longest tasks first (LPT): the grid drains with a short tail.
     std::stable_sort(tasks.begin(), tasks.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
-    // ALS_TASK_ORDER=random (measurement knob): a seeded shuffle of the main launch's tasks instead of LPT
+    // ALS_TASK_ORDER=random / stagger[:W] (measurement knobs): a seeded shuffle of the main launch's tasks, or LPT
+    // windows alternating between its longer and shorter half
     if (const char* env = getenv("ALS_TASK_ORDER")) {
+        if (std::strncmp(env, "stagger", 7) == 0) {
+            // windows of W tasks (W = stagger:<W>, default 1024 = one 4-wave workgroup per CU) alternate between the
+            // longer and the shorter half of the LPT list: co-resident waves of a CU run tasks of different lengths
+            const size_t W = env[7] == ':' ? (size_t)std::max(1, atoi(env + 8)) : 1024;
+            const size_t h = (tasks.size() + 1) / 2;
+            std::vector<Task> out;
+            out.reserve(tasks.size());
+            size_t ia = 0, ib = h;
+            while (ia < h || ib < tasks.size()) {
+                for (size_t q = 0; q < W && ia < h; ++q) out.push_back(tasks[ia++]);
+                for (size_t q = 0; q < W && ib < tasks.size(); ++q) out.push_back(tasks[ib++]);
+            }
+            tasks.swap(out);
+        }
         if (std::strcmp(env, "random") == 0) {
             uint64_t x = 0x9e3779b97f4a7c15ull;
             for (size_t i = tasks.size(); i > 1; --i) {
@@ -531,6 +559,7 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
         // row (< 2^24) and the offset (< 2^32) must fit, also when ALS_PRESPLIT=1 forces the path
         if (n_opp_rows + 1 >= (1 << 24) || sb > (int64_t)UINT32_MAX) ps = false;
         blk.presplit = ps;
+        blk.rat_exact16 = rat_exact16;
         if (ps && (size_t)sb > e->split_bytes) {
             (void)hipFree(e->d_split);
             e->d_split = nullptr;
@@ -650,7 +679,7 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
             return fail(ALS_ERR_OUT_OF_MEMORY, "in-block upload: %s", hipGetErrorString(st));
         }
     }
-    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat);
+    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat, ratings_exact16(ratings, nnz));
 }
 
 int als_set_block_coo(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows, int64_t nnz,
@@ -669,7 +698,7 @@ int als_set_block_coo(als_engine* e, int side, int64_t n_rows, int64_t row_offse
     const int code = cfk::build_block_device(rows, cols, ratings, nnz, n_rows, n_opp_rows, e->stream, deg, begin,
                                              &d_col, &d_rat, err);
     if (code != ALS_OK) return fail(code, "als_set_block_coo: %s", err.c_str());
-    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat);
+    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat, ratings_exact16(ratings, nnz));
 }
 
 int als_alloc_factors(als_engine* e, int side, int64_t n_total_rows) {
@@ -854,7 +883,7 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
         // converts it, later chunks reuse the conversion
         if (first_chunk) {
             const int64_t n_floats = (b.n_opp_rows + 1) * (int64_t)e->kp;
-            HIP_TRY(cfk::launch_absmax((const float*)opp.ptr, n_floats, e->d_amax, e->stream));
+            HIP_TRY(cfk::launch_absmax((const float*)opp.ptr, n_floats, e->kp, e->d_amax, e->stream));
             HIP_TRY(cfk::launch_presplit(e->kp, (const float*)opp.ptr, e->d_split, b.n_opp_rows + 1, e->d_amax,
                                          e->stream));
         }
@@ -863,12 +892,22 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
         a.rat_lo_off = b.nnz_padded / 2;
         a.col_ps = b.d_col_ps;
         a.amax = e->d_amax;
+        a.rat_exact16 = b.rat_exact16 ? 1 : 0;
     }
     a.queue = e->d_queue;
+    a.pc_stats = e->d_pc_stats;
     if (b.presplit && e->pipelined)
         HIP_TRY(cfk::launch_solve_pc(e->kp, a, e->cu_count, e->stream));
     else
         HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.presplit, false));
+    if (b.presplit) {
+        // the range guard's fallback: the same tasks on the fp32 table with the on-the-fly split, a launch whose
+        // waves exit at once unless the opposite table is out of the pre-split's range (cfk::presplit_ok)
+        cfk::SolveArgs f = a;
+        f.presplit_fallback = 1;
+        f.grid_cap = 4 * e->cu_count;
+        HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, f, e->stream, false, false));
+    }
     if (side_dual) HIP_TRY(hipStreamWaitEvent(e->side_stream, e->fork, 0));
     for (int c = 0; c < 3; ++c)
         if (dl.n[c] > 0) {
@@ -1291,3 +1330,20 @@ int als_block_stats(const als_engine* e, int side, int64_t* n_tasks, int64_t* n_
 }
 
 }  // extern "C"
+
+#ifdef CFK_DEBUG_KNOBS
+// Debug build only (not in include/als.h): present iff the work-dropping / fault-injection knobs are compiled in
+// (bench.py refuses a library that exports it, whatever its path).
+extern "C" int als_debug_knobs_compiled(void) { return 1; }
+// Debug build only (not in include/als.h): read (and with reset, zero) the pipelined launch's cycle accounting,
+// cfk::PC_STAT_N counters (tools/kbench.py --pc-stats).
+extern "C" int als_debug_pc_stats(als_engine* e, unsigned long long* out, int reset) {
+    if (int r = check_engine(e)) return r;
+    if (!e->d_pc_stats) return fail(ALS_ERR_STATE, "no pipelined-launch statistics");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(hipMemcpy(out, e->d_pc_stats, cfk::PC_STAT_N * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (reset) HIP_TRY(hipMemset(e->d_pc_stats, 0, cfk::PC_STAT_N * sizeof(unsigned long long)));
+    return ALS_OK;
+}
+#endif

@@ -66,9 +66,15 @@ struct SolveArgs {
     int32_t rows_per_chunk; // chunk-major slots (als_set_row_layout): 0 = factor row row_offset + row, else
     int64_t chunk_stride;   //   row_offset + (row / rows_per_chunk) * chunk_stride + row % rows_per_chunk
     int64_t rat_lo_off;     // presplit: words from the rh pairs to the rm pairs (nnz_padded / 2)
-    const uint32_t* amax;   // presplit: bits of the opposite table's largest |x| (als_absmax): the split scale
+    const uint32_t* amax;   // presplit: range statistics of the opposite table (als_absmax): [0] bits of its largest
+                            //   |x| (the split scale), [1] ~bits of its smallest nonzero row maximum
+    int32_t presplit_fallback;  // the on-the-fly split launch guarding a pre-split half: it runs only when the table
+                                //   is out of the pre-split's range (presplit_ok(amax) false), else exits at once
     int64_t scratch_slabs;  // generic path: workgroup slabs in `partials` (its Gram when it does not fit in LDS)
-    int* queue;             // pipelined launch (als_solve_pc): next task index (zeroed by launch_solve_pc)
+    int* queue;             // pipelined launch (als_solve_pc): PC_QUEUE_INTS task counters (zeroed by launch_solve_pc)
+    unsigned long long* pc_stats;   // debug build only (else null): PC_STAT_* cycle counters of the pipelined launch
+    int32_t rat_exact16;    // presplit: every rating is exact in fp16 (|r| <= 2048): r = rh, rm = 0
+    int32_t grid_cap;       // workgroups of a grid-stride launch (the range guard's fallback): CUs x 4
     int32_t extra_lds;      // diagnostics (debug build's ALS_DEBUG_EXTRA_LDS, else 0): unused dynamic LDS per workgroup
 };
 // Factor row of local row `row` under the block's slot layout (wave-uniform: scalar arithmetic, once per task).
@@ -84,6 +90,14 @@ constexpr int INTEGRITY_WORDS = 4;
 // Slot value of an integrity record written by the pipelined launch (als_solve_pc) when a wave's hand-off wait ran
 // out of time (a protocol failure, not a partial slot).
 constexpr int32_t PC_TIMEOUT_SLOT = -2;
+// Task queue of the pipelined launch: PC_STREAMS counters (stream x = tasks x, x + PC_STREAMS, ...), one 128-B line
+// each, PC_CHUNK stream positions per atomic; SolveArgs::queue holds PC_QUEUE_INTS ints.
+constexpr int PC_STREAMS = 8, PC_QSTRIDE = 32, PC_CHUNK = 8;
+constexpr int PC_QUEUE_INTS = PC_STREAMS * PC_QSTRIDE;
+// Debug-build cycle accounting of the pipelined launch (s_memtime, summed over waves): Gram waves' Gram cycles and
+// cycles waiting for a free slot, solver waves' solve cycles and idle (polling) cycles, systems solved, tasks.
+enum { PC_STAT_GRAM = 0, PC_STAT_GRAM_WAIT, PC_STAT_SOLVE, PC_STAT_SOLVE_IDLE, PC_STAT_SOLVES, PC_STAT_TASKS,
+       PC_STAT_T_SETUP, PC_STAT_T_SCALE, PC_STAT_T_FACTOR, PC_STAT_T_SUBST, PC_STAT_T_END, PC_STAT_N = 16 };
 // Diagnostic: skip the k x k solve after the Gram (stores the Gram diagonal instead) -- used by
 // tools/kbench.py to split a launch's time into Gram and solve. Only the debug build (CFK_DEBUG_KNOBS) can set
 // these flags; the product library never does.
@@ -137,10 +151,10 @@ hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s);
 // the presplit Gram stages in LDS: row r = presplit_row_bytes(kp) = 4 kp bytes (the fp32 row's size) at r * 4 kp =
 // two planes (h, m) of 2 kp bytes, plane position 16 b + j (b = 0..kp/16-1, j = 0..15) holding feature (kp/16) j + b
 // scaled by 2^s, so the 16 values one transposed LDS read hands to a 16-lane group (features (kp/16) j + b,
-// j = 0..15) are 32 contiguous bytes. launch_absmax writes the table's largest |x| (bits) to *amax first (zeroed
+// j = 0..15) are 32 contiguous bytes. launch_absmax writes the table's range statistics to amax[0..1] first (zeroed
 // here, on the stream); the presplit kernel and the Gram derive s from it (als_kernels.hip, split_exp).
 __host__ __device__ constexpr int presplit_row_bytes(int kp) { return 4 * kp; }
-hipError_t launch_absmax(const float* src, int64_t n_floats, uint32_t* amax, hipStream_t s);
+hipError_t launch_absmax(const float* src, int64_t n_floats, int kp, uint32_t* amax /* 2 words */, hipStream_t s);
 hipError_t launch_presplit(int kp, const float* src, void* dst, int64_t n_rows, const uint32_t* amax, hipStream_t s);
 // padded column indices -> the per-block order of the presplit gather (n_entries = nnz_padded)
 hipError_t launch_pack_cols_ps(const int32_t* col, int32_t* dst, int64_t n_entries, hipStream_t s);

@@ -622,6 +622,10 @@ __host__ __device__ constexpr int la_item_I(int C, int P, int t) {   // -1: the 
 #ifndef CFK_PS64_WAVES
 #define CFK_PS64_WAVES 4
 #endif
+// One-kernel pre-split launch: the RHS by v_dot2_f32_f16 instead of 2 C MFMA tiles (gram_presplit's RHS mode)
+#ifndef CFK_PS_DOT2
+#define CFK_PS_DOT2 0
+#endif
 // Pipelined launch: the solver waves' issue priority (s_setprio) and their sweep column broadcasts (1: lane swaps,
 // the shorter latency; 0: ds_bpermute)
 #ifndef CFK_PC_PRIO
@@ -715,9 +719,11 @@ struct RowResidual {
 // DUAL: the system is the entry Gram of a short row (als_solve_dual): unknown 16b + j = the row's entry at
 // physical position 16b + j, real when that entry exists (padding entries get an identity row), and the
 // solution alpha goes to buf[16b + j] (read by the caller after a wave_sync) instead of a factor row.
+// marks (debug build's pipelined-launch accounting, else null): shader clock after the scaling, the
+// factorisation, the first substitution, and at the end.
 template <int C, bool DUAL = false, bool FORCE_SWAP = false, class TT, class KT>
 __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc)[C], float* buf, const Task& tk,
-                                            const SolveArgs& a, int lane) {
+                                            const SolveArgs& a, int lane, uint64_t* marks = nullptr) {
     const int g = lane >> 4, j = lane & 15;
     float* out = (float*)a.out + factor_row(a.row_offset, a.rows_per_chunk, a.chunk_stride, tk.row) * (int64_t)(16 * C);
     auto is_real = [&](int b) { return DUAL ? logical_entry(16 * b + j) < tk.nent : C * j + b < a.k; };
@@ -789,6 +795,7 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 #pragma unroll
     for (int b = 0; b < C; ++b) b0[b] = col_sum(rhs_acc[b]) * scol[b];
 
+    if (marks) marks[0] = __builtin_amdgcn_s_memtime();
     // ---- factorisation (matrix part only) ----
     float nrd_min = -1.f;
     constexpr bool SWAPC = FORCE_SWAP || 16 * C >= CFK_COL_SWAP;
@@ -914,8 +921,10 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
             }
         });
     };
+    if (marks) marks[1] = __builtin_amdgcn_s_memtime();
     float x[C];
     solve_vec(b0, x);
+    if (marks) marks[2] = __builtin_amdgcn_s_memtime();
     // Well-conditioned systems skip the refinement step: every pivot of the scaled (unit-diagonal) system is a
     // Schur-complement diagonal in (0, 1]; when the smallest is >= a.refine_min_pivot the block factorisation's
     // error is already below the reference's own fp32 LU error. The test is wave-uniform.
@@ -924,6 +933,7 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 #pragma unroll
         for (int b = 0; b < C; ++b) xs[b] = x[b] * scol[b];
         emit(xs);
+        if (marks) marks[3] = __builtin_amdgcn_s_memtime();
         return;
     }
     if (a.flags & SOLVE_FLAG_SKIP_REFINE) {   // diagnostics only
@@ -1021,6 +1031,7 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 #pragma unroll
     for (int b = 0; b < C; ++b) xs[b] = (x[b] + dx[b]) * scol[b];
     emit(xs);
+    if (marks) marks[3] = __builtin_amdgcn_s_memtime();
 }
 
 // Waves (tasks) per workgroup of the MFMA kernel: 4, or 2 at KP = 128, whose 72 KB of per-wave LDS tiles
@@ -1028,26 +1039,56 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 template <int KP>
 constexpr int mfma_waves() { return WAVES; }
 
-// Largest |x| of a table (the pre-split scale, split_exp): grid-stride over 16-B vectors, workgroup max, one
-// vector-memory atomicMax per workgroup on the bits (non-negative floats order as unsigned integers). *out is zeroed
-// before the launch.
-__global__ __launch_bounds__(256) void als_absmax(const u32x4* __restrict__ src, int64_t n4, uint32_t* __restrict__ out) {
-    uint32_t m = 0;
+// Range statistics of a table for the pre-split Gram, from the bits of |x| (non-negative floats order as unsigned
+// integers): out[0] = the largest |x| (the split scale, split_exp), out[1] = ~(the smallest nonzero row maximum) (a
+// max of complements is a min; 0 = no nonzero row). Grid-stride over 16-B vectors, vpr vectors per row (a row's
+// vectors are consecutive lanes of one wave: the grid stride is a multiple of 64), workgroup reduction, one
+// vector-memory atomicMax per workgroup and word. out[0..1] are zeroed before the launch.
+__global__ __launch_bounds__(256) void als_absmax(const u32x4* __restrict__ src, int64_t n4, int vpr,
+                                                  uint32_t* __restrict__ out) {
+    uint32_t m = 0, rmin = 0xffffffffu;
     const int64_t stride = (int64_t)gridDim.x * 256;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
-        const u32x4 v = src[i] & 0x7fffffffu;
-        m = max(max(m, max(v[0], v[1])), max(v[2], v[3]));
+    for (int64_t i0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); i0 < n4; i0 += stride) {
+        const int64_t i = i0 + (threadIdx.x & 63);
+        uint32_t v = 0;
+        if (i < n4) {
+            const u32x4 x = src[i] & 0x7fffffffu;
+            v = max(max(x[0], x[1]), max(x[2], x[3]));
+        }
+        m = max(m, v);
+        for (int o = 1; o < vpr; o <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));   // the row's maximum
+        if (v != 0 && i < n4) rmin = min(rmin, v);
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    for (int o = 32; o > 0; o >>= 1) {
+        m = max(m, (uint32_t)__shfl_xor((int)m, o));
+        rmin = min(rmin, (uint32_t)__shfl_xor((int)rmin, o));
+    }
     // one atomic per workgroup: thousands of same-address atomics serialise (53 us for the 4.5 MB M table)
-    __shared__ uint32_t wm[4];
-    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __shared__ uint32_t wm[4], wr[4];
+    if ((threadIdx.x & 63) == 0) {
+        wm[threadIdx.x >> 6] = m;
+        wr[threadIdx.x >> 6] = rmin;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         m = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
+        rmin = min(min(wr[0], wr[1]), min(wr[2], wr[3]));
         if (m != 0) atomicMax(out, m);
+        if (rmin != 0xffffffffu) atomicMax(out + 1, ~rmin);
     }
+}
+// The pre-split (table-wide scale, two fp16 terms) keeps ~22 significant bits for values within 2^-17 of the table's
+// largest |x| and falls toward the fp16 subnormal floor below; it serves a half only when every nonzero row's
+// maximum is within PRESPLIT_RANGE of the table's. Otherwise that half's Gram runs on the fp32 table with the
+// on-the-fly three-term bf16 split (an 8-bit exponent per value): the pre-split kernels exit at once and the
+// guarded on-the-fly launch after them does the work (SolveArgs::presplit_fallback).
+constexpr float PRESPLIT_RANGE = 65536.f;
+__device__ __forceinline__ bool presplit_ok(const uint32_t* st) {
+    const uint32_t mx = st[0], rc = st[1];
+    if (mx >= 0x7f800000u) return false;   // inf / NaN in the table: the fp32 path propagates it as the reference would
+    if (rc == 0) return true;              // no nonzero row
+    return __uint_as_float(mx) <= PRESPLIT_RANGE * __uint_as_float(~rc);
 }
 
 // fp32 table -> fp16 h/m planes (presplit_row_bytes(KP) per row, als_internal.h) at the table's scale 2^s: thread
@@ -1104,11 +1145,12 @@ __device__ __forceinline__ void store_partial(const SolveArgs& a, const Task& tk
 
 // Pre-split fp16 Gram of one FULL / PARTIAL task into acc (tiles, RHS) and E (the diagonal tiles' h m^T terms,
 // folded by the caller), in the table's units. img: the wave's 2 C KB LDS image (1-KB aligned); buf: its KP floats.
-// LEAN (the pipelined KP = 128 Gram role, whose wave has half the register file): E unused -- a diagonal tile takes
-// hh + hm + mh like the others (3 MFMAs) -- and the RHS by v_dot2_f32_f16 on the operand registers (the lane's h/m
-// pairs of its 8 entries times the rh/rm pairs, per-lane partial sums that solve_tiles' col_sum completes) instead
-// of 2 C RHS MFMA tiles: 32 + 24 accumulator registers fewer, 108 MFMAs per block at KP = 128 instead of 116.
-template <int KP, bool LEAN = false>
+// NOE: E unused -- a diagonal tile takes hh + hm + mh like the others (3 MFMAs; 32 accumulator registers fewer at
+// KP = 128). RHS (0: the 2 C RHS MFMA tiles; 1 / 2: v_dot2_f32_f16 on the operand registers -- the lane's h/m pairs
+// of its 8 entries times the rh and rm pairs (1) or the rh pairs alone when every rating is exact in fp16 (2),
+// per-lane partial sums reduced over the 4 lane rows at the end): 2 C MFMAs per block fewer, 8 C or 4 C VALU more.
+// The pipelined KP = 128 Gram role, whose wave has half the register file, needs both (108 MFMAs per block).
+template <int KP, bool NOE = false, int RHS = 0>
 __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk, MfmaAcc<KP / 16>& acc,
                                               f32x4 (&E)[KP / 16], unsigned char* img, float* buf, int lane) {
     constexpr int C = KP / 16;
@@ -1127,23 +1169,24 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
     constexpr int NPL = 2;                 // planes h, m
     const char* tbase = (const char*)a.opp_split;
     const int sc = split_exp(*a.amax);     // the table's scale 2^sc (wave-uniform scalar load)
-    constexpr int NR = LEAN ? 1 : C;       // RHS MFMA tiles (LEAN: none)
+    constexpr bool DOT2 = RHS != 0;
+    constexpr int NR = DOT2 ? 1 : C;       // RHS MFMA tiles (dot2 RHS: none)
     f32x4 racc[NR];
 #pragma unroll
     for (int b = 0; b < NR; ++b) racc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float rsum[C];                         // LEAN: per-lane RHS partial sums
+    float rsum[C];                         // dot2 RHS: per-lane partial sums
 #pragma unroll
     for (int b = 0; b < C; ++b) rsum[b] = 0.f;
     // the block's MFMAs on operands P[plane h/m][feature block b] (entries 8g..8g+7 of feature C j + b as
-    // fp16 pairs) and the fp16 rating pairs R of the same entries (rh or rm by the lane's column; LEAN: rh in R,
-    // rm in Rm, every lane)
+    // fp16 pairs) and the fp16 rating pairs R of the same entries (rh or rm by the lane's column; dot2 RHS: rh in
+    // R, rm in Rm, every lane)
     auto mfma_block = [&](const u32x4 (&P)[NPL][C], const u32x4& R, const u32x4& Rm) {
 #pragma unroll
         for (int b1 = 0; b1 < C; ++b1)
 #pragma unroll
             for (int b2 = b1; b2 < C; ++b2) {
                 f32x4 t = acc.g[tile_index<C>(b1, b2)];
-                if (CFK_DIAG_SYM && !LEAN && b1 == b2) {
+                if (CFK_DIAG_SYM && !NOE && b1 == b2) {
                     E[b1] = mfma_f16(P[0][b1], P[1][b1], E[b1]);
                 } else {
                     t = mfma_f16(P[0][b1], P[1][b2], t);
@@ -1152,14 +1195,16 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
                 t = mfma_f16(P[0][b1], P[0][b2], t);
                 acc.g[tile_index<C>(b1, b2)] = t;
             }
-        if constexpr (LEAN) {
+        if constexpr (DOT2) {
 #pragma unroll
             for (int b = 0; b < C; ++b) {
                 float v = rsum[b];
 #pragma unroll
                 for (int w = 0; w < 4; ++w) {
-                    v = dot2_f16(P[1][b][w], Rm[w], v);
-                    v = dot2_f16(P[0][b][w], Rm[w], v);
+                    if constexpr (RHS == 1) {
+                        v = dot2_f16(P[1][b][w], Rm[w], v);
+                        v = dot2_f16(P[0][b][w], Rm[w], v);
+                    }
                     v = dot2_f16(P[1][b][w], R[w], v);
                     v = dot2_f16(P[0][b][w], R[w], v);
                 }
@@ -1239,12 +1284,12 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
     if (nblk > 0) {
         const int lastb = nblk - 1;
         const i32x4* cp = (const i32x4*)(a.col_ps + tk.begin) + r8;          // + 8 per block
-        // rating pairs of the lane's column half: rh (columns 0-7) or rm (columns 8-15); LEAN: rh, and rm in Rmn
-        const u32x4* rp = (const u32x4*)(a.rat_pk + ((j >= 8 && !LEAN) ? a.rat_lo_off : 0) + (tk.begin >> 1)) + g;
+        // rating pairs of the lane's column half: rh (columns 0-7) or rm (columns 8-15); dot2 RHS: rh, rm in Rmn
+        const u32x4* rp = (const u32x4*)(a.rat_pk + ((j >= 8 && !DOT2) ? a.rat_lo_off : 0) + (tk.begin >> 1)) + g;
         const u32x4* rpm = (const u32x4*)(a.rat_pk + a.rat_lo_off + (tk.begin >> 1)) + g;
         i32x4 cv = cp[0];
         u32x4 Rn = rp[0], Rmn = {0u, 0u, 0u, 0u};
-        if constexpr (LEAN) Rmn = rpm[0];
+        if constexpr (RHS == 1) Rmn = rpm[0];
         issue(cv);
         cv = cp[8 * min(1, lastb)];
         for (int b = 0; b < nblk; ++b) {
@@ -1260,7 +1305,7 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
             if (b < lastb) issue(cv);
             cv = cp[8 * min(b + 2, lastb)];
             Rn = rp[4 * min(b + 1, lastb)];
-            if constexpr (LEAN) Rmn = rpm[4 * min(b + 1, lastb)];
+            if constexpr (RHS == 1) Rmn = rpm[4 * min(b + 1, lastb)];
             __builtin_amdgcn_sched_barrier(0);
             mfma_block(P, R, Rm);
             __builtin_amdgcn_sched_barrier(0);
@@ -1271,7 +1316,13 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
     for (int t = 0; t < Acc::NT; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc.g[t][r] = ldexpf(acc.g[t][r], -2 * sc);
-    if constexpr (LEAN) {   // the other paths' per-lane RHS layout: the whole sum in row g = 0, zeros elsewhere
+    if constexpr (!NOE) {
+#pragma unroll
+        for (int b = 0; b < C; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) E[b][r] = ldexpf(E[b][r], -2 * sc);
+    }
+    if constexpr (DOT2) {   // the other paths' per-lane RHS layout: the whole sum in row g = 0, zeros elsewhere
 #pragma unroll
         for (int b = 0; b < C; ++b) {
             const float v = ldexpf(col_sum(rsum[b]), -sc);
@@ -1279,10 +1330,6 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
         }
         return;
     }
-#pragma unroll
-    for (int b = 0; b < C; ++b)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) E[b][r] = ldexpf(E[b][r], -2 * sc);
     // RHS tiles (row i of block b = feature C i + b; column 0 = Y^T rh, column 8 = Y^T rm) -> the per-lane
     // partial layout of the other paths: lane (0, j) holds feature C j + b, the other rows zero (col_sum
     // restores it)
@@ -1304,7 +1351,10 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
 
 // REDUCE = true: the launch of a half's REDUCE tasks (sum of partial slots + solve), compiled apart from the
 // gather kernel so neither carries the other's code and registers.
-template <int KP, int MINW, bool SPLIT, bool PRESPLIT = false, bool REDUCE = false>
+// GRIDLOOP: a grid-stride loop over the tasks (the range guard's fallback launch, whose grid is capped: when the
+// pre-split serves the half, as it nearly always does, its waves exit without a full-size grid's dispatch cost).
+template <int KP, int MINW, bool SPLIT, bool PRESPLIT = false, bool REDUCE = false, bool NOE = false, int RHS = 0,
+          bool GRIDLOOP = false>
 __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(SolveArgs a) {
     constexpr int C = KP / 16;
     constexpr int NW = mfma_waves<KP>();
@@ -1323,451 +1373,463 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
     (void)stage_lds;
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tid = blockIdx.x * NW + wave;
-    if (tid >= a.n_tasks) return;   // wave-uniform; no workgroup barriers are used below
-    const Task tk = load_task(a.tasks + tid);
-    float* buf = sbuf[wave];
+    // the table-range guard (presplit_ok): a pre-split launch serves the half only in range, its guarded on-the-fly
+    // fallback only out of range (one scalar load per wave; the other launch's waves exit here)
+    if constexpr (!REDUCE && SPLIT) {
+        if (PRESPLIT ? !presplit_ok(a.amax) : (a.presplit_fallback && presplit_ok(a.amax))) return;
+    }
+    // one task per wave (wave-uniform; no workgroup barriers are used below)
+    auto task = [&](const int tid) {
+        const Task tk = load_task(a.tasks + tid);
+        float* buf = sbuf[wave];
 
-    const int g = lane >> 4, j = lane & 15;
-    Acc acc;
+        const int g = lane >> 4, j = lane & 15;
+        Acc acc;
 #pragma unroll
-    for (int p = 0; p < Acc::NT; ++p) acc.g[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int p = 0; p < Acc::NT; ++p) acc.g[p] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < C; ++c) acc.rhs[c] = 0.f;
-    f32x4 E[C];   // split paths: h m^T + h l^T of the diagonal tiles (fold_diag)
+        for (int c = 0; c < C; ++c) acc.rhs[c] = 0.f;
+        f32x4 E[C];   // split paths: h m^T + h l^T of the diagonal tiles (fold_diag)
 #pragma unroll
-    for (int c = 0; c < C; ++c) E[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < C; ++c) E[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    float* part = (float*)a.partials;
-    constexpr int SLOT_WORDS = Acc::NWORDS + 1;   // + integrity check word
-    if constexpr (REDUCE) {
-        // Fixed-order sum of the row's partial slots ([word][lane] layout, coalesced), each decoded and checked.
-        bool bad = false;
-        int32_t bad_slot = -1;
-        for (int s = 0; s < tk.nsteps; ++s) {
-            const float* src = part + (int64_t)(tk.slot + s) * (SLOT_WORDS * 64) + lane;
-            SlotCodec cd{slot_key(a.gen, tk.slot + s, lane)};
-            // the whole slot's loads are issued before the first use: left to the scheduler under the KP = 128
-            // register pressure they went out one at a time (load, wait, add: 0.44 ms for 974 rows)
-            float w[SLOT_WORDS];
+        float* part = (float*)a.partials;
+        constexpr int SLOT_WORDS = Acc::NWORDS + 1;   // + integrity check word
+        if constexpr (REDUCE) {
+            // Fixed-order sum of the row's partial slots ([word][lane] layout, coalesced), each decoded and checked.
+            bool bad = false;
+            int32_t bad_slot = -1;
+            for (int s = 0; s < tk.nsteps; ++s) {
+                const float* src = part + (int64_t)(tk.slot + s) * (SLOT_WORDS * 64) + lane;
+                SlotCodec cd{slot_key(a.gen, tk.slot + s, lane)};
+                // the whole slot's loads are issued before the first use: left to the scheduler under the KP = 128
+                // register pressure they went out one at a time (load, wait, add: 0.44 ms for 974 rows)
+                float w[SLOT_WORDS];
 #pragma unroll
-            for (int q = 0; q < SLOT_WORDS; ++q) w[q] = src[q * 64];
-            __builtin_amdgcn_sched_barrier(0);
+                for (int q = 0; q < SLOT_WORDS; ++q) w[q] = src[q * 64];
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int p = 0; p < Acc::NT; ++p)
+                for (int p = 0; p < Acc::NT; ++p)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc.g[p][r] += cd.dec(w[p * 4 + r], p * 4 + r);
+                    for (int r = 0; r < 4; ++r) acc.g[p][r] += cd.dec(w[p * 4 + r], p * 4 + r);
 #pragma unroll
-            for (int c = 0; c < C; ++c) acc.rhs[c] += cd.dec(w[Acc::NT * 4 + c], Acc::NT * 4 + c);
-            const bool ok = cd.check_ok(w[Acc::NWORDS], Acc::NWORDS);
-            if (!ok && !bad) bad_slot = tk.slot + s;
-            bad |= !ok;
-        }
-        report_bad_slot(a.integrity, a.gen, bad_slot, tk.row, bad, lane);
-    } else {
-        // Gather pipeline over blocks of B = 8 sub-steps (32 entries, layout [g][t], see block_position):
-        // lane (g, j) loads the 8 column indices / ratings of its group with two 16-B loads, issued one
-        // block ahead of that block's gathers, which are issued one block ahead of their MFMAs. The loop
-        // body is branch-free, so vmcnt retires in program order with 8 gathers (8 KB per wave) still in
-        // flight under each block's 80 MFMAs.
-        constexpr int B = BLOCK_SUBSTEPS;
-        const float* opp = (const float*)a.opp;
-        const int n = tk.nsteps;
-        const int nblk = (n + B - 1) / B;
-        const int32_t* cb = a.col + tk.begin + g * B;
-        const float* rb = a.rat + tk.begin + g * B;
-        typedef int i32x4 __attribute__((ext_vector_type(4)));
-        struct Idx { i32x4 i[2]; f32x4 r[2]; };
-        auto load_idx = [&](int blk, Idx& x) {
-            const int32_t* c = cb + (int64_t)blk * BLOCK_ENTRIES;
-            const float* r = rb + (int64_t)blk * BLOCK_ENTRIES;
-            x.i[0] = *(const i32x4*)c;
-            x.i[1] = *(const i32x4*)(c + 4);
-            x.r[0] = *(const f32x4*)r;
-            x.r[1] = *(const f32x4*)(r + 4);
-        };
-        // unconditional: padding entries index the sentinel zero row; 32-bit unsigned byte offsets (host-checked:
-        // opposite table <= 4 GiB, e.g. 16.7M rows at k = 64)
-        // wave-uniform table base + 32-bit per-lane byte offsets (row << log2(row bytes), + this lane's piece): the
-        // loads take the saddr form, one v_lshl_add_u32 per gathered row instead of a 64-bit address per lane
-        const char* obase = (const char*)opp;
-        const uint32_t lane_off = (uint32_t)(C * j * sizeof(float));
-        constexpr int ROW_SHIFT = __builtin_ctz(KP * sizeof(float));
-        auto gather = [&](const Idx& x, VT (&y)[B]) {
-#pragma unroll
-            for (int t = 0; t < B; ++t)
-                y[t] = *(const VT*)(obase + (((uint32_t)x.i[t >> 2][t & 3] << ROW_SHIFT) + lane_off));
-        };
-        auto mfma_step = [&](const VT& y, float r) {
-#pragma unroll
-            for (int b1 = 0; b1 < C; ++b1)
-#pragma unroll
-                for (int b2 = b1; b2 < C; ++b2)
-                    acc.g[tile_index<C>(b1, b2)] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                        y[b1], y[b2], acc.g[tile_index<C>(b1, b2)], 0, 0, 0);
-#pragma unroll
-            for (int c = 0; c < C; ++c) acc.rhs[c] += r * y[c];
-        };
-        if constexpr (PRESPLIT) {
-            gram_presplit<KP>(a, tk, acc, E, stage_lds[uni(wave)], buf, lane);
-        } else if constexpr (SPLIT) {
-            // Split-bf16 Gram: one v_mfma_f32_16x16x32_bf16 consumes a whole 32-entry block. Lane (g, j)
-            // holds A[i = j][k = 8g + t] = y_t[C*j + b] (its own gathered piece, component b, entry t of its
-            // group): with the interleaved feature order (f = C*i + b) the operands need no lane movement,
-            // and the accumulators come out in exactly the layout of the f32 path (tile (b1, b2) holds
-            // G[C*i + b1][C*j' + b2]), so the solve, the partial slots and the REDUCE pass are shared.
-            // Padding entries gather the sentinel zero row with rating 0, so the last block needs no mask.
+                for (int c = 0; c < C; ++c) acc.rhs[c] += cd.dec(w[Acc::NT * 4 + c], Acc::NT * 4 + c);
+                const bool ok = cd.check_ok(w[Acc::NWORDS], Acc::NWORDS);
+                if (!ok && !bad) bad_slot = tk.slot + s;
+                bad |= !ok;
+            }
+            report_bad_slot(a.integrity, a.gen, bad_slot, tk.row, bad, lane);
+        } else {
+            // Gather pipeline over blocks of B = 8 sub-steps (32 entries, layout [g][t], see block_position):
+            // lane (g, j) loads the 8 column indices / ratings of its group with two 16-B loads, issued one
+            // block ahead of that block's gathers, which are issued one block ahead of their MFMAs. The loop
+            // body is branch-free, so vmcnt retires in program order with 8 gathers (8 KB per wave) still in
+            // flight under each block's 80 MFMAs.
+            constexpr int B = BLOCK_SUBSTEPS;
+            const float* opp = (const float*)a.opp;
+            const int n = tk.nsteps;
+            const int nblk = (n + B - 1) / B;
+            const int32_t* cb = a.col + tk.begin + g * B;
+            const float* rb = a.rat + tk.begin + g * B;
             typedef int i32x4 __attribute__((ext_vector_type(4)));
-            struct Cols { i32x4 i[2]; };
-            struct Rats { f32x4 r[2]; };
-            auto load_cols = [&](int blk, Cols& x) {
+            struct Idx { i32x4 i[2]; f32x4 r[2]; };
+            auto load_idx = [&](int blk, Idx& x) {
                 const int32_t* c = cb + (int64_t)blk * BLOCK_ENTRIES;
+                const float* r = rb + (int64_t)blk * BLOCK_ENTRIES;
                 x.i[0] = *(const i32x4*)c;
                 x.i[1] = *(const i32x4*)(c + 4);
-            };
-            auto load_rats = [&](int blk, Rats& x) {
-                const float* r = rb + (int64_t)blk * BLOCK_ENTRIES;
                 x.r[0] = *(const f32x4*)r;
                 x.r[1] = *(const f32x4*)(r + 4);
             };
-            auto gather_blk = [&](const Cols& x, VT (&y)[B]) {
+            // unconditional: padding entries index the sentinel zero row; 32-bit unsigned byte offsets (host-checked:
+            // opposite table <= 4 GiB, e.g. 16.7M rows at k = 64)
+            // wave-uniform table base + 32-bit per-lane byte offsets (row << log2(row bytes), + this lane's piece): the
+            // loads take the saddr form, one v_lshl_add_u32 per gathered row instead of a 64-bit address per lane
+            const char* obase = (const char*)opp;
+            const uint32_t lane_off = (uint32_t)(C * j * sizeof(float));
+            constexpr int ROW_SHIFT = __builtin_ctz(KP * sizeof(float));
+            auto gather = [&](const Idx& x, VT (&y)[B]) {
 #pragma unroll
                 for (int t = 0; t < B; ++t)
                     y[t] = *(const VT*)(obase + (((uint32_t)x.i[t >> 2][t & 3] << ROW_SHIFT) + lane_off));
             };
-            auto split_step = [&](const VT (&y)[B], const Rats& x) {
-                u32x4 H[C], M[C], L[C];
-#pragma unroll
-                for (int b = 0; b < C; ++b)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        unsigned h, m, l;
-                        split3(y[2 * q][b], y[2 * q + 1][b], h, m, l);
-                        pin(h);
-                        pin(m);
-                        pin(l);
-                        H[b][q] = h;
-                        M[b][q] = m;
-                        L[b][q] = l;
-                    }
-                if constexpr (CFK_RHS_EARLY) {
-#pragma unroll
-                    for (int t = 0; t < B; ++t)
-#pragma unroll
-                        for (int c = 0; c < C; ++c) acc.rhs[c] += x.r[t >> 2][t & 3] * y[t][c];
-#pragma unroll
-                    for (int c = 0; c < C; ++c) pin(acc.rhs[c]);
-                }
-                // the operands are materialised above (pin: MachineSink ignores sched_barrier), so the MFMA group
-                // below contains no VALU that could overwrite an operand register of an MFMA in flight
-                __builtin_amdgcn_sched_barrier(0);
+            auto mfma_step = [&](const VT& y, float r) {
 #pragma unroll
                 for (int b1 = 0; b1 < C; ++b1)
 #pragma unroll
-                    for (int b2 = b1; b2 < C; ++b2) {
-                        f32x4 t = acc.g[tile_index<C>(b1, b2)];
-                        t = mfma_k32(M[b1], M[b2], t);
-                        if (CFK_DIAG_SYM && b1 == b2) {
-                            f32x4 e = E[b1];
-                            e = mfma_k32(H[b1], L[b1], e);
-                            e = mfma_k32(H[b1], M[b1], e);
-                            E[b1] = e;
-                        } else {
-                            t = mfma_k32(H[b1], L[b2], t);
-                            t = mfma_k32(L[b1], H[b2], t);
-                            t = mfma_k32(H[b1], M[b2], t);
-                            t = mfma_k32(M[b1], H[b2], t);
-                        }
-                        t = mfma_k32(H[b1], H[b2], t);
-                        acc.g[tile_index<C>(b1, b2)] = t;
-                    }
-                MFMA_DRAIN();
-                if constexpr (!CFK_RHS_EARLY) {
+                    for (int b2 = b1; b2 < C; ++b2)
+                        acc.g[tile_index<C>(b1, b2)] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                            y[b1], y[b2], acc.g[tile_index<C>(b1, b2)], 0, 0, 0);
+#pragma unroll
+                for (int c = 0; c < C; ++c) acc.rhs[c] += r * y[c];
+            };
+            if constexpr (PRESPLIT) {
+                gram_presplit<KP, NOE, RHS>(a, tk, acc, E, stage_lds[uni(wave)], buf, lane);
+            } else if constexpr (SPLIT) {
+                // Split-bf16 Gram: one v_mfma_f32_16x16x32_bf16 consumes a whole 32-entry block. Lane (g, j)
+                // holds A[i = j][k = 8g + t] = y_t[C*j + b] (its own gathered piece, component b, entry t of its
+                // group): with the interleaved feature order (f = C*i + b) the operands need no lane movement,
+                // and the accumulators come out in exactly the layout of the f32 path (tile (b1, b2) holds
+                // G[C*i + b1][C*j' + b2]), so the solve, the partial slots and the REDUCE pass are shared.
+                // Padding entries gather the sentinel zero row with rating 0, so the last block needs no mask.
+                typedef int i32x4 __attribute__((ext_vector_type(4)));
+                struct Cols { i32x4 i[2]; };
+                struct Rats { f32x4 r[2]; };
+                auto load_cols = [&](int blk, Cols& x) {
+                    const int32_t* c = cb + (int64_t)blk * BLOCK_ENTRIES;
+                    x.i[0] = *(const i32x4*)c;
+                    x.i[1] = *(const i32x4*)(c + 4);
+                };
+                auto load_rats = [&](int blk, Rats& x) {
+                    const float* r = rb + (int64_t)blk * BLOCK_ENTRIES;
+                    x.r[0] = *(const f32x4*)r;
+                    x.r[1] = *(const f32x4*)(r + 4);
+                };
+                auto gather_blk = [&](const Cols& x, VT (&y)[B]) {
 #pragma unroll
                     for (int t = 0; t < B; ++t)
+                        y[t] = *(const VT*)(obase + (((uint32_t)x.i[t >> 2][t & 3] << ROW_SHIFT) + lane_off));
+                };
+                auto split_step = [&](const VT (&y)[B], const Rats& x) {
+                    u32x4 H[C], M[C], L[C];
 #pragma unroll
-                        for (int c = 0; c < C; ++c) acc.rhs[c] += x.r[t >> 2][t & 3] * y[t][c];
-                }
-            };
-            // Two blocks per trip with ping-pong buffers (no register rotation): column indices are loaded two
-            // blocks ahead of their gathers' use, gathers and ratings one block ahead of their MFMAs.
-            // Invariant at the loop top: Y0/R0 in flight for block b, I1 = columns of b+1, I0 = columns of b+2.
-            if (C > 4 && CFK_K128_INTERLEAVE && nblk > 0) {
-                // KP = 128, one wave per SIMD: no second wave hides the split VALU behind this wave's MFMAs, so
-                // the wave interleaves them itself. The tiles are issued column by column (column c = tiles
-                // (b1 <= c, c): 6c + 4 MFMAs), and the split of feature block c + 1 -- the only new operand
-                // column c + 1 needs -- plus a share of the RHS FMAs run in the issue gaps of column c's MFMAs
-                // (an MFMA holds vector issue for 8 of its 16 cycles: two VALU per gap). Column 7's gaps split
-                // feature block 0 of the next block. No operand register dies before column 7 and all of them
-                // are kept allocated past the closing drain (keep_alive), so no VALU result can land in a
-                // register an MFMA in flight still reads. Same products, same accumulation order per tile and
-                // per RHS component as split_step: bitwise equal results.
-                Cols I0, I1;
-                Rats R0, R1;
-                VT Y0[B], Y1[B];
-                u32x4 H[C], M[C], L[C];
-                const int lastb = nblk - 1;
-                auto split_feat = [&](const VT (&y)[B], int c, u32x4& h4, u32x4& m4, u32x4& l4) {
+                    for (int b = 0; b < C; ++b)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        unsigned h, m, l;
-                        split3(y[2 * q][c], y[2 * q + 1][c], h, m, l);
-                        h4[q] = h;
-                        m4[q] = m;
-                        l4[q] = l;
+                        for (int q = 0; q < 4; ++q) {
+                            unsigned h, m, l;
+                            split3(y[2 * q][b], y[2 * q + 1][b], h, m, l);
+                            pin(h);
+                            pin(m);
+                            pin(l);
+                            H[b][q] = h;
+                            M[b][q] = m;
+                            L[b][q] = l;
+                        }
+                    if constexpr (CFK_RHS_EARLY) {
+#pragma unroll
+                        for (int t = 0; t < B; ++t)
+#pragma unroll
+                            for (int c = 0; c < C; ++c) acc.rhs[c] += x.r[t >> 2][t & 3] * y[t][c];
+#pragma unroll
+                        for (int c = 0; c < C; ++c) pin(acc.rhs[c]);
                     }
-                };
-                auto keep_alive = [&]() {
+                    // the operands are materialised above (pin: MachineSink ignores sched_barrier), so the MFMA group
+                    // below contains no VALU that could overwrite an operand register of an MFMA in flight
+                    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int b = 0; b < C; ++b) asm volatile("" ::"v"(H[b]), "v"(M[b]), "v"(L[b]));
-                };
-                // one block: y/x = this block, yn = the next block (its feature block 0 is split here) when NEXT
-                auto block = [&](const VT (&y)[B], const Rats& x, const VT (&yn)[B], auto next_) {
-                    constexpr bool NEXT = decltype(next_)::value;
-                    u32x4 hn, mn, ln;
-                    static_for<0, C>([&](auto C_) {
-                        constexpr int c = decltype(C_)::value;
+                    for (int b1 = 0; b1 < C; ++b1)
 #pragma unroll
-                        for (int b1 = 0; b1 <= c; ++b1) {
-                            f32x4 t = acc.g[tile_index<C>(b1, c)];
-                            t = mfma_k32(M[b1], M[c], t);
-                            if (CFK_DIAG_SYM && b1 == c) {
+                        for (int b2 = b1; b2 < C; ++b2) {
+                            f32x4 t = acc.g[tile_index<C>(b1, b2)];
+                            t = mfma_k32(M[b1], M[b2], t);
+                            if (CFK_DIAG_SYM && b1 == b2) {
                                 f32x4 e = E[b1];
                                 e = mfma_k32(H[b1], L[b1], e);
                                 e = mfma_k32(H[b1], M[b1], e);
                                 E[b1] = e;
                             } else {
-                                t = mfma_k32(H[b1], L[c], t);
-                                t = mfma_k32(L[b1], H[c], t);
-                                t = mfma_k32(H[b1], M[c], t);
-                                t = mfma_k32(M[b1], H[c], t);
+                                t = mfma_k32(H[b1], L[b2], t);
+                                t = mfma_k32(L[b1], H[b2], t);
+                                t = mfma_k32(H[b1], M[b2], t);
+                                t = mfma_k32(M[b1], H[b2], t);
                             }
-                            t = mfma_k32(H[b1], H[c], t);
-                            acc.g[tile_index<C>(b1, c)] = t;
+                            t = mfma_k32(H[b1], H[b2], t);
+                            acc.g[tile_index<C>(b1, b2)] = t;
                         }
-                        if constexpr (c + 1 < C) split_feat(y, c + 1, H[c + 1], M[c + 1], L[c + 1]);
-                        // RHS components 0-1 in column 5's gaps, 2-4 in column 6's, 5-7 in column 7's
-                        constexpr int r0 = c == 5 ? 0 : c == 6 ? 2 : c == 7 ? 5 : C;
-                        constexpr int r1 = c == 5 ? 2 : c == 6 ? 5 : c == 7 ? 8 : C;
-#pragma unroll
-                        for (int f = r0; f < r1; ++f)
-#pragma unroll
-                            for (int t = 0; t < B; ++t) acc.rhs[f] += x.r[t >> 2][t & 3] * y[t][f];
-                        if constexpr (NEXT && c == C - 1) split_feat(yn, 0, hn, mn, ln);
-                        static_for<0, 6 * c + 4>([&](auto) {
-                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-                            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // 2 VALU
-                        });
-                        __builtin_amdgcn_sched_barrier(0);
-                    });
                     MFMA_DRAIN();
-                    keep_alive();
-                    __builtin_amdgcn_sched_barrier(0);
-                    if constexpr (NEXT) {
-                        H[0] = hn;
-                        M[0] = mn;
-                        L[0] = ln;
+                    if constexpr (!CFK_RHS_EARLY) {
+#pragma unroll
+                        for (int t = 0; t < B; ++t)
+#pragma unroll
+                            for (int c = 0; c < C; ++c) acc.rhs[c] += x.r[t >> 2][t & 3] * y[t][c];
                     }
                 };
-                using Yes = std::integral_constant<bool, true>;
-                using No = std::integral_constant<bool, false>;
-                // one block per trip, staging rotated (two blocks per trip with ping-pong buffers made the
-                // register allocator shuffle the 144 accumulator registers at every back edge)
-                load_cols(0, I0);
-                load_cols(min(1, lastb), I1);
-                gather_blk(I0, Y0);
-                load_rats(0, R0);
-                split_feat(Y0, 0, H[0], M[0], L[0]);
-                for (int b = 0; b < lastb; ++b) {
-                    gather_blk(I1, Y1);
-                    load_rats(b + 1, R1);
-                    load_cols(min(b + 2, lastb), I1);
-                    __builtin_amdgcn_sched_barrier(0);
-                    block(Y0, R0, Y1, Yes{});
+                // Two blocks per trip with ping-pong buffers (no register rotation): column indices are loaded two
+                // blocks ahead of their gathers' use, gathers and ratings one block ahead of their MFMAs.
+                // Invariant at the loop top: Y0/R0 in flight for block b, I1 = columns of b+1, I0 = columns of b+2.
+                if (C > 4 && CFK_K128_INTERLEAVE && nblk > 0) {
+                    // KP = 128, one wave per SIMD: no second wave hides the split VALU behind this wave's MFMAs, so
+                    // the wave interleaves them itself. The tiles are issued column by column (column c = tiles
+                    // (b1 <= c, c): 6c + 4 MFMAs), and the split of feature block c + 1 -- the only new operand
+                    // column c + 1 needs -- plus a share of the RHS FMAs run in the issue gaps of column c's MFMAs
+                    // (an MFMA holds vector issue for 8 of its 16 cycles: two VALU per gap). Column 7's gaps split
+                    // feature block 0 of the next block. No operand register dies before column 7 and all of them
+                    // are kept allocated past the closing drain (keep_alive), so no VALU result can land in a
+                    // register an MFMA in flight still reads. Same products, same accumulation order per tile and
+                    // per RHS component as split_step: bitwise equal results.
+                    Cols I0, I1;
+                    Rats R0, R1;
+                    VT Y0[B], Y1[B];
+                    u32x4 H[C], M[C], L[C];
+                    const int lastb = nblk - 1;
+                    auto split_feat = [&](const VT (&y)[B], int c, u32x4& h4, u32x4& m4, u32x4& l4) {
 #pragma unroll
-                    for (int t = 0; t < B; ++t) Y0[t] = Y1[t];
-                    R0 = R1;
-                }
-                block(Y0, R0, Y1, No{});
-            } else if (C > 4 && nblk > 0) {
-                // KP = 128 (1 wave per SIMD, 144 accumulator registers): one staging set, rotated
-                Cols Ic, In;
-                Rats Rc, Rn;
-                VT Yc[B], Yn[B];
-                const int lastb = nblk - 1;
-                load_cols(0, Ic);
-                load_cols(min(1, lastb), In);
-                gather_blk(Ic, Yc);
-                load_rats(0, Rc);
-                for (int b = 0; b < lastb; ++b) {
-                    gather_blk(In, Yn);
-                    load_rats(b + 1, Rn);
-                    load_cols(min(b + 2, lastb), In);
-                    __builtin_amdgcn_sched_barrier(0);
+                        for (int q = 0; q < 4; ++q) {
+                            unsigned h, m, l;
+                            split3(y[2 * q][c], y[2 * q + 1][c], h, m, l);
+                            h4[q] = h;
+                            m4[q] = m;
+                            l4[q] = l;
+                        }
+                    };
+                    auto keep_alive = [&]() {
+#pragma unroll
+                        for (int b = 0; b < C; ++b) asm volatile("" ::"v"(H[b]), "v"(M[b]), "v"(L[b]));
+                    };
+                    // one block: y/x = this block, yn = the next block (its feature block 0 is split here) when NEXT
+                    auto block = [&](const VT (&y)[B], const Rats& x, const VT (&yn)[B], auto next_) {
+                        constexpr bool NEXT = decltype(next_)::value;
+                        u32x4 hn, mn, ln;
+                        static_for<0, C>([&](auto C_) {
+                            constexpr int c = decltype(C_)::value;
+#pragma unroll
+                            for (int b1 = 0; b1 <= c; ++b1) {
+                                f32x4 t = acc.g[tile_index<C>(b1, c)];
+                                t = mfma_k32(M[b1], M[c], t);
+                                if (CFK_DIAG_SYM && b1 == c) {
+                                    f32x4 e = E[b1];
+                                    e = mfma_k32(H[b1], L[b1], e);
+                                    e = mfma_k32(H[b1], M[b1], e);
+                                    E[b1] = e;
+                                } else {
+                                    t = mfma_k32(H[b1], L[c], t);
+                                    t = mfma_k32(L[b1], H[c], t);
+                                    t = mfma_k32(H[b1], M[c], t);
+                                    t = mfma_k32(M[b1], H[c], t);
+                                }
+                                t = mfma_k32(H[b1], H[c], t);
+                                acc.g[tile_index<C>(b1, c)] = t;
+                            }
+                            if constexpr (c + 1 < C) split_feat(y, c + 1, H[c + 1], M[c + 1], L[c + 1]);
+                            // RHS components 0-1 in column 5's gaps, 2-4 in column 6's, 5-7 in column 7's
+                            constexpr int r0 = c == 5 ? 0 : c == 6 ? 2 : c == 7 ? 5 : C;
+                            constexpr int r1 = c == 5 ? 2 : c == 6 ? 5 : c == 7 ? 8 : C;
+#pragma unroll
+                            for (int f = r0; f < r1; ++f)
+#pragma unroll
+                                for (int t = 0; t < B; ++t) acc.rhs[f] += x.r[t >> 2][t & 3] * y[t][f];
+                            if constexpr (NEXT && c == C - 1) split_feat(yn, 0, hn, mn, ln);
+                            static_for<0, 6 * c + 4>([&](auto) {
+                                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+                                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // 2 VALU
+                            });
+                            __builtin_amdgcn_sched_barrier(0);
+                        });
+                        MFMA_DRAIN();
+                        keep_alive();
+                        __builtin_amdgcn_sched_barrier(0);
+                        if constexpr (NEXT) {
+                            H[0] = hn;
+                            M[0] = mn;
+                            L[0] = ln;
+                        }
+                    };
+                    using Yes = std::integral_constant<bool, true>;
+                    using No = std::integral_constant<bool, false>;
+                    // one block per trip, staging rotated (two blocks per trip with ping-pong buffers made the
+                    // register allocator shuffle the 144 accumulator registers at every back edge)
+                    load_cols(0, I0);
+                    load_cols(min(1, lastb), I1);
+                    gather_blk(I0, Y0);
+                    load_rats(0, R0);
+                    split_feat(Y0, 0, H[0], M[0], L[0]);
+                    for (int b = 0; b < lastb; ++b) {
+                        gather_blk(I1, Y1);
+                        load_rats(b + 1, R1);
+                        load_cols(min(b + 2, lastb), I1);
+                        __builtin_amdgcn_sched_barrier(0);
+                        block(Y0, R0, Y1, Yes{});
+#pragma unroll
+                        for (int t = 0; t < B; ++t) Y0[t] = Y1[t];
+                        R0 = R1;
+                    }
+                    block(Y0, R0, Y1, No{});
+                } else if (C > 4 && nblk > 0) {
+                    // KP = 128 (1 wave per SIMD, 144 accumulator registers): one staging set, rotated
+                    Cols Ic, In;
+                    Rats Rc, Rn;
+                    VT Yc[B], Yn[B];
+                    const int lastb = nblk - 1;
+                    load_cols(0, Ic);
+                    load_cols(min(1, lastb), In);
+                    gather_blk(Ic, Yc);
+                    load_rats(0, Rc);
+                    for (int b = 0; b < lastb; ++b) {
+                        gather_blk(In, Yn);
+                        load_rats(b + 1, Rn);
+                        load_cols(min(b + 2, lastb), In);
+                        __builtin_amdgcn_sched_barrier(0);
+                        split_step(Yc, Rc);
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int t = 0; t < B; ++t) Yc[t] = Yn[t];
+                        Rc = Rn;
+                    }
                     split_step(Yc, Rc);
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int t = 0; t < B; ++t) Yc[t] = Yn[t];
-                    Rc = Rn;
+                } else if (MINW >= 3 && nblk > 0) {
+                    // three waves per SIMD: one gather buffer, columns one block ahead
+                    Cols I;
+                    Rats R;
+                    VT Y[B];
+                    const int lastb = nblk - 1;
+                    load_cols(0, I);
+                    for (int b = 0; b < nblk; ++b) {
+                        gather_blk(I, Y);
+                        load_rats(b, R);
+                        load_cols(min(b + 1, lastb), I);
+                        __builtin_amdgcn_sched_barrier(0);
+                        split_step(Y, R);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                } else if (nblk > 0) {
+                    Cols I0, I1;
+                    Rats R0, R1;
+                    VT Y0[B], Y1[B];
+                    const int lastb = nblk - 1;
+                    load_cols(0, I0);
+                    load_cols(min(1, lastb), I1);
+                    gather_blk(I0, Y0);
+                    load_rats(0, R0);
+                    load_cols(min(2, lastb), I0);
+                    int b = 0;
+                    for (; b + 2 < nblk; b += 2) {
+                        gather_blk(I1, Y1);
+                        load_rats(b + 1, R1);
+                        load_cols(min(b + 3, lastb), I1);
+                        __builtin_amdgcn_sched_barrier(0);
+                        split_step(Y0, R0);
+                        __builtin_amdgcn_sched_barrier(0);
+                        gather_blk(I0, Y0);
+                        load_rats(b + 2, R0);
+                        load_cols(min(b + 4, lastb), I0);
+                        __builtin_amdgcn_sched_barrier(0);
+                        split_step(Y1, R1);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    if (nblk - b == 2) {
+                        gather_blk(I1, Y1);
+                        load_rats(b + 1, R1);
+                        __builtin_amdgcn_sched_barrier(0);
+                        split_step(Y0, R0);
+                        split_step(Y1, R1);
+                    } else {
+                        split_step(Y0, R0);
+                    }
                 }
-                split_step(Yc, Rc);
-            } else if (MINW >= 3 && nblk > 0) {
-                // three waves per SIMD: one gather buffer, columns one block ahead
-                Cols I;
-                Rats R;
-                VT Y[B];
-                const int lastb = nblk - 1;
-                load_cols(0, I);
-                for (int b = 0; b < nblk; ++b) {
-                    gather_blk(I, Y);
-                    load_rats(b, R);
-                    load_cols(min(b + 1, lastb), I);
-                    __builtin_amdgcn_sched_barrier(0);
-                    split_step(Y, R);
-                    __builtin_amdgcn_sched_barrier(0);
+            } else if constexpr (C > 4) {
+                // KP = 128: 288 MFMAs per block, so half a block of prefetch (4 gathered rows per lane in
+                // flight) covers the gather latency and halves the staging registers (the 36 accumulator
+                // tiles already take 144). Stage = 4 sub-steps = one 16-B index/rating vector per lane.
+                constexpr int H = B / 2;
+                auto gather_half = [&](const Idx& x, auto h_, VT (&y)[H]) {
+                    constexpr int h = decltype(h_)::value;
+#pragma unroll
+                    for (int t = 0; t < H; ++t)
+                        y[t] = *(const VT*)(obase + (((uint32_t)x.i[h][t] << ROW_SHIFT) + lane_off));
+                };
+                using H0 = std::integral_constant<int, 0>;
+                using H1 = std::integral_constant<int, 1>;
+                if (nblk > 0) {
+                    Idx x_c, x_n;
+                    VT y_c[H], y_n[H];
+                    load_idx(0, x_c);
+                    load_idx(nblk > 1 ? 1 : 0, x_n);
+                    gather_half(x_c, H0{}, y_c);
+                    for (int b = 0; b + 1 < nblk; ++b) {
+                        gather_half(x_c, H1{}, y_n);
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int t = 0; t < H; ++t) mfma_step(y_c[t], x_c.r[0][t]);
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int t = 0; t < H; ++t) y_c[t] = y_n[t];
+                        Idx x_nn;
+                        load_idx(b + 2 < nblk ? b + 2 : nblk - 1, x_nn);   // clamped: always a valid address
+                        gather_half(x_n, H0{}, y_n);
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int t = 0; t < H; ++t) mfma_step(y_c[t], x_c.r[1][t]);
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int t = 0; t < H; ++t) y_c[t] = y_n[t];
+                        x_c = x_n;
+                        x_n = x_nn;
+                    }
+                    const int last = n - (nblk - 1) * B;
+                    gather_half(x_c, H1{}, y_n);
+#pragma unroll
+                    for (int t = 0; t < H; ++t)
+                        if (t < last) mfma_step(y_c[t], x_c.r[0][t]);     // wave-uniform
+#pragma unroll
+                    for (int t = 0; t < H; ++t)
+                        if (H + t < last) mfma_step(y_n[t], x_c.r[1][t]);
                 }
             } else if (nblk > 0) {
-                Cols I0, I1;
-                Rats R0, R1;
-                VT Y0[B], Y1[B];
-                const int lastb = nblk - 1;
-                load_cols(0, I0);
-                load_cols(min(1, lastb), I1);
-                gather_blk(I0, Y0);
-                load_rats(0, R0);
-                load_cols(min(2, lastb), I0);
-                int b = 0;
-                for (; b + 2 < nblk; b += 2) {
-                    gather_blk(I1, Y1);
-                    load_rats(b + 1, R1);
-                    load_cols(min(b + 3, lastb), I1);
-                    __builtin_amdgcn_sched_barrier(0);
-                    split_step(Y0, R0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    gather_blk(I0, Y0);
-                    load_rats(b + 2, R0);
-                    load_cols(min(b + 4, lastb), I0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    split_step(Y1, R1);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                if (nblk - b == 2) {
-                    gather_blk(I1, Y1);
-                    load_rats(b + 1, R1);
-                    __builtin_amdgcn_sched_barrier(0);
-                    split_step(Y0, R0);
-                    split_step(Y1, R1);
-                } else {
-                    split_step(Y0, R0);
-                }
-            }
-        } else if constexpr (C > 4) {
-            // KP = 128: 288 MFMAs per block, so half a block of prefetch (4 gathered rows per lane in
-            // flight) covers the gather latency and halves the staging registers (the 36 accumulator
-            // tiles already take 144). Stage = 4 sub-steps = one 16-B index/rating vector per lane.
-            constexpr int H = B / 2;
-            auto gather_half = [&](const Idx& x, auto h_, VT (&y)[H]) {
-                constexpr int h = decltype(h_)::value;
-#pragma unroll
-                for (int t = 0; t < H; ++t)
-                    y[t] = *(const VT*)(obase + (((uint32_t)x.i[h][t] << ROW_SHIFT) + lane_off));
-            };
-            using H0 = std::integral_constant<int, 0>;
-            using H1 = std::integral_constant<int, 1>;
-            if (nblk > 0) {
                 Idx x_c, x_n;
-                VT y_c[H], y_n[H];
+                VT y_c[B], y_n[B];
                 load_idx(0, x_c);
                 load_idx(nblk > 1 ? 1 : 0, x_n);
-                gather_half(x_c, H0{}, y_c);
+                gather(x_c, y_c);
                 for (int b = 0; b + 1 < nblk; ++b) {
-                    gather_half(x_c, H1{}, y_n);
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int t = 0; t < H; ++t) mfma_step(y_c[t], x_c.r[0][t]);
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int t = 0; t < H; ++t) y_c[t] = y_n[t];
                     Idx x_nn;
                     load_idx(b + 2 < nblk ? b + 2 : nblk - 1, x_nn);   // clamped: always a valid address
-                    gather_half(x_n, H0{}, y_n);
+                    gather(x_n, y_n);
+                    // keep the prefetch above the MFMAs: without this the scheduler sinks the gathers below
+                    // them (saving registers) and every block waits out a full memory latency
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int t = 0; t < H; ++t) mfma_step(y_c[t], x_c.r[1][t]);
+                    for (int t = 0; t < B; ++t) mfma_step(y_c[t], x_c.r[t >> 2][t & 3]);
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int t = 0; t < H; ++t) y_c[t] = y_n[t];
+                    for (int t = 0; t < B; ++t) y_c[t] = y_n[t];
                     x_c = x_n;
                     x_n = x_nn;
                 }
-                const int last = n - (nblk - 1) * B;
-                gather_half(x_c, H1{}, y_n);
+                const int last = n - (nblk - 1) * B;     // sub-steps with real entries in the last block
 #pragma unroll
-                for (int t = 0; t < H; ++t)
-                    if (t < last) mfma_step(y_c[t], x_c.r[0][t]);     // wave-uniform
-#pragma unroll
-                for (int t = 0; t < H; ++t)
-                    if (H + t < last) mfma_step(y_n[t], x_c.r[1][t]);
+                for (int t = 0; t < B; ++t)
+                    if (t < last) mfma_step(y_c[t], x_c.r[t >> 2][t & 3]);   // wave-uniform
             }
-        } else if (nblk > 0) {
-            Idx x_c, x_n;
-            VT y_c[B], y_n[B];
-            load_idx(0, x_c);
-            load_idx(nblk > 1 ? 1 : 0, x_n);
-            gather(x_c, y_c);
-            for (int b = 0; b + 1 < nblk; ++b) {
-                Idx x_nn;
-                load_idx(b + 2 < nblk ? b + 2 : nblk - 1, x_nn);   // clamped: always a valid address
-                gather(x_n, y_n);
-                // keep the prefetch above the MFMAs: without this the scheduler sinks the gathers below
-                // them (saving registers) and every block waits out a full memory latency
-                __builtin_amdgcn_sched_barrier(0);
+        }
+
+        if constexpr (SPLIT && CFK_DIAG_SYM && !NOE) {
+            if constexpr (!REDUCE) fold_diag<C>(acc, E, lane);
+        }
+
+        if (!REDUCE && tk.kind == TASK_PARTIAL) {
+            store_partial<C>(a, tk, acc, lane);
+            return;
+        }
+
+        if (a.flags & SOLVE_FLAG_SKIP_SOLVE) {   // diagnostics (kbench): Gram only
+            float* out = (float*)a.out + factor_row(a.row_offset, a.rows_per_chunk, a.chunk_stride, tk.row) * (int64_t)KP;
+            if (lane < 16) {
 #pragma unroll
-                for (int t = 0; t < B; ++t) mfma_step(y_c[t], x_c.r[t >> 2][t & 3]);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int t = 0; t < B; ++t) y_c[t] = y_n[t];
-                x_c = x_n;
-                x_n = x_nn;
+                for (int b = 0; b < C; ++b) out[C * lane + b] = acc.g[tile_index<C>(b, b)][0] + acc.rhs[b];
             }
-            const int last = n - (nblk - 1) * B;     // sub-steps with real entries in the last block
-#pragma unroll
-            for (int t = 0; t < B; ++t)
-                if (t < last) mfma_step(y_c[t], x_c.r[t >> 2][t & 3]);   // wave-uniform
+            return;
         }
-    }
-
-    if constexpr (SPLIT && CFK_DIAG_SYM) {
-        if constexpr (!REDUCE) fold_diag<C>(acc, E, lane);
-    }
-
-    if (!REDUCE && tk.kind == TASK_PARTIAL) {
-        store_partial<C>(a, tk, acc, lane);
-        return;
-    }
-
-    if (a.flags & SOLVE_FLAG_SKIP_SOLVE) {   // diagnostics (kbench): Gram only
-        float* out = (float*)a.out + factor_row(a.row_offset, a.rows_per_chunk, a.chunk_stride, tk.row) * (int64_t)KP;
-        if (lane < 16) {
+        if constexpr (TILES_LDS) {
+            LdsTiles T{tiles_lds[wave] + (CFK_LDS_B128 ? 4 : 1) * lane};
+            RegStore<C> A0;
 #pragma unroll
-            for (int b = 0; b < C; ++b) out[C * lane + b] = acc.g[tile_index<C>(b, b)][0] + acc.rhs[b];
+            for (int p = 0; p < Acc::NT; ++p) T.put(p, acc.g[p]);
+            solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
+        } else if constexpr (PRESPLIT && !REDUCE) {
+            RegTiles<C> T{acc.g};
+            RowResidual A0;
+            solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
+        } else {
+            RegTiles<C> T{acc.g};
+            RegStore<C> A0;
+            solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
         }
-        return;
-    }
-    if constexpr (TILES_LDS) {
-        LdsTiles T{tiles_lds[wave] + (CFK_LDS_B128 ? 4 : 1) * lane};
-        RegStore<C> A0;
-#pragma unroll
-        for (int p = 0; p < Acc::NT; ++p) T.put(p, acc.g[p]);
-        solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
-    } else if constexpr (PRESPLIT && !REDUCE) {
-        RegTiles<C> T{acc.g};
-        RowResidual A0;
-        solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
+    };
+    if constexpr (GRIDLOOP) {
+        for (int tid = blockIdx.x * NW + wave; tid < a.n_tasks; tid += gridDim.x * NW) task(tid);
     } else {
-        RegTiles<C> T{acc.g};
-        RegStore<C> A0;
-        solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
+        const int tid = blockIdx.x * NW + wave;
+        if (tid < a.n_tasks) task(tid);
     }
 }
 
@@ -1790,6 +1852,24 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
 // cycle. Every wait is bounded in time (PC_WAIT_TICKS of the 100 MHz real-time counter); a wave that runs out
 // records it in the integrity record (slot PC_TIMEOUT_SLOT) and leaves, so the grid always drains.
 constexpr int PC_FREE = 0, PC_WRITING = 1, PC_FULL = 2, PC_READING = 3;
+// debug build: shader-clock accounting of the roles (a.pc_stats); product build: nothing
+#ifdef CFK_DEBUG_KNOBS
+#define PC_CLOCK() __builtin_amdgcn_s_memtime()
+#else
+#define PC_CLOCK() 0ull
+#endif
+__device__ __forceinline__ void pc_stats_add(const SolveArgs& a, int i0, uint64_t v0, int i1, uint64_t v1, int i2,
+                                             uint64_t v2, int lane) {
+#ifdef CFK_DEBUG_KNOBS
+    if (a.pc_stats && lane == 0) {
+        atomicAdd(a.pc_stats + i0, (unsigned long long)v0);
+        atomicAdd(a.pc_stats + i1, (unsigned long long)v1);
+        atomicAdd(a.pc_stats + i2, (unsigned long long)v2);
+    }
+#else
+    (void)a; (void)i0; (void)v0; (void)i1; (void)v1; (void)i2; (void)v2; (void)lane;
+#endif
+}
 constexpr uint64_t PC_WAIT_TICKS = 200000000ull;   // 2 s
 __device__ __forceinline__ uint64_t pc_now() { return __builtin_amdgcn_s_memrealtime(); }
 
@@ -1849,6 +1929,7 @@ __device__ __forceinline__ SolveArgs uniform_args(const SolveArgs& in) {
     a.amax = unip(in.amax);
     a.scratch_slabs = uni64(in.scratch_slabs);
     a.queue = unip(in.queue);
+    a.pc_stats = unip(in.pc_stats);
     a.extra_lds = uni(in.extra_lds);
     return a;
 }
@@ -1861,6 +1942,9 @@ __device__ __attribute__((noinline)) void pc_solve_slot(SolveArgs a_in, int sl_i
     using L = PcLds<KP, NG, NS, NSLOT>;
     constexpr int C = KP / 16;
     using Acc = MfmaAcc<C>;
+#ifdef CFK_DEBUG_KNOBS
+    const uint64_t c_in = __builtin_amdgcn_s_memtime();
+#endif
     const SolveArgs a = uniform_args(a_in);
     const int sl = uni(sl_in), wave = uni(wave_in);
     const int lane = __lane_id(), g = lane >> 4, j = lane & 15;
@@ -1884,7 +1968,21 @@ __device__ __attribute__((noinline)) void pc_solve_slot(SolveArgs a_in, int sl_i
     }
     RegTiles<C> T{acc.g};
     RowResidual A0;
+#ifdef CFK_DEBUG_KNOBS
+    uint64_t mk[4] = {c_in, c_in, c_in, c_in};
+    const uint64_t c_pre = __builtin_amdgcn_s_memtime();
+    solve_tiles<C, false, CFK_PC_SWAP != 0>(T, A0, acc.rhs, L::sbuf(wave), tk, a, lane, mk);
+    // setup (args, slot, task), scaling, factorisation, substitution, emit / refinement
+    if (a.pc_stats && lane == 0) {
+        atomicAdd(a.pc_stats + PC_STAT_T_SETUP, (unsigned long long)(c_pre - c_in));
+        atomicAdd(a.pc_stats + PC_STAT_T_SCALE, (unsigned long long)(mk[0] - c_pre));
+        atomicAdd(a.pc_stats + PC_STAT_T_FACTOR, (unsigned long long)(mk[1] - mk[0]));
+        atomicAdd(a.pc_stats + PC_STAT_T_SUBST, (unsigned long long)(mk[2] - mk[1]));
+        atomicAdd(a.pc_stats + PC_STAT_T_END, (unsigned long long)(mk[3] - mk[2]));
+    }
+#else
     solve_tiles<C, false, CFK_PC_SWAP != 0>(T, A0, acc.rhs, L::sbuf(wave), tk, a, lane);
+#endif
 }
 
 template <int KP, int NG, int NS, int NSLOT>
@@ -1897,6 +1995,7 @@ __global__ __launch_bounds__(64 * (NG + NS), 1) void als_solve_pc(SolveArgs a) {
     int* ndone = state + NSLOT;
 
     const int wave = uni((int)(threadIdx.x >> 6)), lane0 = threadIdx.x & 63;
+    if (!presplit_ok(a.amax)) return;   // out of the pre-split's range: the guarded fallback launch solves the half
     if (threadIdx.x < NSLOT) state[threadIdx.x] = PC_FREE;
     if (threadIdx.x == 0) *ndone = 0;
     __syncthreads();   // the only workgroup barrier: every wave passes it before any wave waits on another
@@ -1908,14 +2007,26 @@ __global__ __launch_bounds__(64 * (NG + NS), 1) void als_solve_pc(SolveArgs a) {
         // ---- Gram role ----
         unsigned char* img = L::img(wave);
         float* buf = L::sbuf(wave);
-        int tl = 0;
-        if (lane0 == 0) tl = atomicAdd(a.queue, 1);
-        int t = uni(tl);
-        while (t < a.n_tasks) {
+        uint64_t st_gram = 0, st_wait = 0, st_tasks = 0;   // debug-build cycle accounting (PC_CLOCK)
+        // task stream x = the workgroup's XCD (workgroups are dealt to the 8 XCDs round-robin): tasks x, x + 8, ...
+        // (still longest first), taken PC_CHUNK stream positions per vector atomic on the stream's own counter --
+        // one same-address atomic per task serialised the k = 64 user half at ~75 M atomics/s (5.1 ms)
+        const int x = (int)(blockIdx.x % PC_STREAMS);
+        int* qx = a.queue + x * PC_QSTRIDE;
+        const int nx = a.n_tasks > x ? (a.n_tasks - x + PC_STREAMS - 1) / PC_STREAMS : 0;
+        int pos = 0, end = 0;   // the wave's current chunk of stream positions
+        while (true) {
+            if (pos == end) {
+                int b = 0;
+                if (lane0 == 0) b = atomicAdd(qx, PC_CHUNK);
+                pos = uni(b);
+                end = pos + PC_CHUNK;
+            }
+            if (pos >= nx) break;
+            const int t = x + PC_STREAMS * pos++;
+            const uint64_t c0 = PC_CLOCK();
             // a fresh lane id per task: nothing lane-derived is hoisted out of the loop and kept live across it
             const int lane = opaque(lane0);
-            int tn = 0;   // the next task index, fetched under this task's Gram
-            if (lane == 0) tn = atomicAdd(a.queue, 1);
             const Task tk = load_task(a.tasks + t);
             Acc acc;
 #pragma unroll
@@ -1925,9 +2036,13 @@ __global__ __launch_bounds__(64 * (NG + NS), 1) void als_solve_pc(SolveArgs a) {
             f32x4 E[C];
 #pragma unroll
             for (int c = 0; c < C; ++c) E[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-            constexpr bool LEAN = KP == 128;
-            gram_presplit<KP, LEAN>(a, tk, acc, E, img, buf, lane);
-            if constexpr (CFK_DIAG_SYM && !LEAN) fold_diag<C>(acc, E, lane);
+            constexpr bool NOE = KP == 128;   // the KP = 128 Gram role fits its half of the register file so
+            constexpr int RHS = KP == 128 ? 1 : 0;   // (rh and rm pairs: one instantiation per role layout)
+            gram_presplit<KP, NOE, RHS>(a, tk, acc, E, img, buf, lane);
+            if constexpr (CFK_DIAG_SYM && !NOE) fold_diag<C>(acc, E, lane);
+            const uint64_t c1 = PC_CLOCK();
+            st_gram += c1 - c0;
+            ++st_tasks;
             if (tk.kind == TASK_PARTIAL) {
                 store_partial<C>(a, tk, acc, lane);
             } else {
@@ -1951,6 +2066,7 @@ __global__ __launch_bounds__(64 * (NG + NS), 1) void als_solve_pc(SolveArgs a) {
                     if (sl >= 0 || pc_now() - t0 > PC_WAIT_TICKS) break;
                     __builtin_amdgcn_s_sleep(1);
                 }
+                st_wait += PC_CLOCK() - c1;
                 if (sl < 0) {   // no solver freed a slot in PC_WAIT_TICKS: record and leave (the grid drains)
                     report_bad_slot(a.integrity, a.gen, PC_TIMEOUT_SLOT, tk.row, true, lane);
                     break;
@@ -1968,9 +2084,9 @@ __global__ __launch_bounds__(64 * (NG + NS), 1) void als_solve_pc(SolveArgs a) {
                     __hip_atomic_store(&state[sl], PC_FULL, __ATOMIC_RELEASE, WG);
                 }
             }
-            t = uni(tn);
         }
         if (lane0 == 0) __hip_atomic_fetch_add(ndone, 1, __ATOMIC_RELEASE, WG);
+        pc_stats_add(a, PC_STAT_GRAM, st_gram, PC_STAT_GRAM_WAIT, st_wait, PC_STAT_TASKS, st_tasks, lane0);
         return;
     }
 
@@ -1981,6 +2097,7 @@ __global__ __launch_bounds__(64 * (NG + NS), 1) void als_solve_pc(SolveArgs a) {
     // the solve is a latency-bound chain beside a Gram wave with independent MFMAs to spare: it issues first
     if constexpr (CFK_PC_PRIO > 0) __builtin_amdgcn_s_setprio(CFK_PC_PRIO);
     uint64_t t0 = pc_now();
+    uint64_t st_solve = 0, st_idle = 0, st_n = 0, c_idle = PC_CLOCK();
     while (true) {
         int cl = -1, fin = 0;
         if (lane0 == 0) {
@@ -2006,9 +2123,16 @@ __global__ __launch_bounds__(64 * (NG + NS), 1) void als_solve_pc(SolveArgs a) {
             __builtin_amdgcn_s_sleep(2);
             continue;
         }
+        const uint64_t c0 = PC_CLOCK();
+        st_idle += c0 - c_idle;
         pc_solve_slot<KP, NG, NS, NSLOT>(a, sl, wave);
+        c_idle = PC_CLOCK();
+        st_solve += c_idle - c0;
+        ++st_n;
         t0 = pc_now();
     }
+    st_idle += PC_CLOCK() - c_idle;
+    pc_stats_add(a, PC_STAT_SOLVE, st_solve, PC_STAT_SOLVE_IDLE, st_idle, PC_STAT_SOLVES, st_n, lane0);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -2322,6 +2446,9 @@ __global__ __launch_bounds__(256) void als_solve_generic(SolveArgs a, int kp, in
     T* G = G_LDS ? (T*)gsmem : scratch + (int64_t)blockIdx.x * slab;   // packed lower triangle, tri(i, j)
     T* stage = (T*)gsmem + (G_LDS ? ((ntri + 1) & ~(int64_t)1) : 0); // batch x kp gathered rows
     __shared__ T vec[1024 + 1];                                         // RHS / solution (kp <= 1024) + pivot
+    // fp64: the refinement step's residual / correction and per-entry residuals of a batch (batch <= 64)
+    __shared__ T res[std::is_same<T, double>::value ? 1024 : 1];
+    __shared__ T tb[std::is_same<T, double>::value ? 64 : 1];
     const T* opp = (const T*)a.opp;
     auto tri_ = [](int64_t i, int64_t j) { return i * (i + 1) / 2 + j; };
     for (int task = blockIdx.x; task < a.n_tasks; task += gridDim.x) {
@@ -2383,18 +2510,55 @@ __global__ __launch_bounds__(256) void als_solve_generic(SolveArgs a, int kp, in
             }
             __syncthreads();
         }
-        for (int j = 0; j < kp; ++j) {   // forward: L y = b (y over vec)
-            const T y = vec[j] / G[tri_(j, j)];
+        auto chol_solve = [&](T* v) {   // v <- (L L^T)^{-1} v
+            for (int j = 0; j < kp; ++j) {   // forward: L y = v
+                const T y = v[j] / G[tri_(j, j)];
+                __syncthreads();
+                if (tid == 0) v[j] = y;
+                for (int i = j + 1 + tid; i < kp; i += 256) v[i] -= G[tri_(i, j)] * y;
+                __syncthreads();
+            }
+            for (int j = kp - 1; j >= 0; --j) {   // backward: L^T x = y
+                const T x = v[j] / G[tri_(j, j)];
+                __syncthreads();
+                if (tid == 0) v[j] = x;
+                for (int i = tid; i < j; i += 256) v[i] -= G[tri_(j, i)] * x;
+                __syncthreads();
+            }
+        };
+        chol_solve(vec);
+        if constexpr (std::is_same<T, double>::value) {
+            // fp64 parity mode: one step of iterative refinement, x += (L L^T)^{-1} (b - A x), with the residual
+            // formed from the rows themselves (A x = Y^T (Y x) + lambda n x; the triangle now holds L):
+            // b - A x = sum_e y_e (r_e - y_e . x) - lambda n x. The Cholesky's own error on the near-zero elements
+            // of a wide solution (~cond * eps of the row norm) drops by about cond.
+            for (int i = tid; i < kp; i += 256) res[i] = -(i < a.k ? reg : T(1)) * vec[i];
             __syncthreads();
-            if (tid == 0) vec[j] = y;
-            for (int i = j + 1 + tid; i < kp; i += 256) vec[i] -= G[tri_(i, j)] * y;
-            __syncthreads();
-        }
-        for (int j = kp - 1; j >= 0; --j) {   // backward: L^T x = y
-            const T x = vec[j] / G[tri_(j, j)];
-            __syncthreads();
-            if (tid == 0) vec[j] = x;
-            for (int i = tid; i < j; i += 256) vec[i] -= G[tri_(j, i)] * x;
+            const int wv = tid >> 6, ln = tid & 63;
+            for (int base = 0; base < n; base += batch) {
+                const int nb = min(batch, n - base);
+                for (int x = tid; x < nb * kp; x += 256) {
+                    const int e = x / kp, f = x - e * kp;
+                    stage[x] = opp[(int64_t)a.col[tk.begin + base + e] * kp + f];
+                }
+                __syncthreads();
+                for (int e = wv; e < nb; e += 4) {   // t_e = r_e - y_e . x, one wave per entry
+                    T d = T(0);
+                    for (int f = ln; f < kp; f += 64) d += stage[e * kp + f] * vec[f];
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
+                    if (ln == 0) tb[e] = (T)a.rat[tk.begin + base + e] - d;
+                }
+                __syncthreads();
+                for (int i = tid; i < kp; i += 256) {
+                    T acc = res[i];
+                    for (int e = 0; e < nb; ++e) acc += stage[e * kp + i] * tb[e];
+                    res[i] = acc;
+                }
+                __syncthreads();
+            }
+            chol_solve(res);
+            for (int i = tid; i < kp; i += 256) vec[i] += res[i];
             __syncthreads();
         }
         for (int i = tid; i < kp; i += 256) out[i] = i < a.k ? vec[i] : T(0);
@@ -2483,10 +2647,23 @@ hipError_t launch_solve_t(const SolveArgs& a, hipStream_t s, bool reduce) {
         constexpr int nw = mfma_waves<KP>();
         const unsigned grid = (unsigned)((a.n_tasks + nw - 1) / nw);
         const size_t dyn = (size_t)a.extra_lds;   // debug build only: unused LDS per workgroup (occupancy sweeps)
-        if (reduce)   // one REDUCE kernel per KP: the partial slots have the same layout on every Gram path
+        constexpr bool SPLIT = P == Path::MFMA_SPLIT;
+        if (reduce) {   // one REDUCE kernel per KP: the partial slots have the same layout on every Gram path
             als_solve_mfma<KP, MINW, false, false, true><<<grid, 64 * nw, 0, s>>>(a);
-        else
-            als_solve_mfma<KP, MINW, P == Path::MFMA_SPLIT, PRESPLIT><<<grid, 64 * nw, dyn, s>>>(a);
+        } else if constexpr (!PRESPLIT && SPLIT) {
+            if (a.presplit_fallback)   // the range guard's fallback: grid-stride over a capped grid
+                als_solve_mfma<KP, MINW, true, false, false, false, 0, true>
+                    <<<std::min<unsigned>(grid, (unsigned)std::max(1, a.grid_cap)), 64 * nw, dyn, s>>>(a);
+            else
+                als_solve_mfma<KP, MINW, true, false><<<grid, 64 * nw, dyn, s>>>(a);
+        } else if constexpr (PRESPLIT && CFK_PS_DOT2) {   // RHS by dot2 (on the rh pairs alone when exact)
+            if (a.rat_exact16)
+                als_solve_mfma<KP, MINW, SPLIT, PRESPLIT, false, false, 2><<<grid, 64 * nw, dyn, s>>>(a);
+            else
+                als_solve_mfma<KP, MINW, SPLIT, PRESPLIT, false, false, 1><<<grid, 64 * nw, dyn, s>>>(a);
+        } else {
+            als_solve_mfma<KP, MINW, SPLIT, PRESPLIT><<<grid, 64 * nw, dyn, s>>>(a);
+        }
     } else {
         hipError_t e = ensure_dyn_lds((const void*)als_solve_valu<T, KP>, bytes);
         if (e != hipSuccess) return e;
@@ -2589,14 +2766,14 @@ hipError_t launch_pack_ratings(const float* rat, uint32_t* dst, int64_t n_pairs,
     als_pack_ratings<<<(unsigned)((n_pairs + 255) / 256), 256, 0, s>>>(rat, dst, n_pairs);
     return hipGetLastError();
 }
-hipError_t launch_absmax(const float* src, int64_t n_floats, uint32_t* amax, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(amax, 0, sizeof(uint32_t), s);
+hipError_t launch_absmax(const float* src, int64_t n_floats, int kp, uint32_t* amax, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(amax, 0, 2 * sizeof(uint32_t), s);
     if (e != hipSuccess || n_floats <= 0) return e;
-    if (n_floats % 4) return hipErrorInvalidValue;   // whole KP-wide rows
+    if (n_floats % kp || kp % 4 || kp / 4 > 64 || (kp / 4 & (kp / 4 - 1))) return hipErrorInvalidValue;   // whole rows
     const int64_t n4 = n_floats / 4;
     // >= 8 vectors per thread, at most 512 workgroups (= atomics)
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n4 + 2047) / 2048, 512));
-    als_absmax<<<(unsigned)blocks, 256, 0, s>>>((const u32x4*)src, n4, amax);
+    als_absmax<<<(unsigned)blocks, 256, 0, s>>>((const u32x4*)src, n4, kp / 4, amax);
     return hipGetLastError();
 }
 hipError_t launch_presplit(int kp, const float* src, void* dst, int64_t n_rows, const uint32_t* amax, hipStream_t s) {
@@ -2627,7 +2804,7 @@ hipError_t launch_pc_t(const SolveArgs& a, int cu_count, hipStream_t s) {
 // Pipelined pre-split launch (als_solve_pc): grid = min(CUs, enough workgroups for the tasks); a.queue zeroed here.
 hipError_t launch_solve_pc(int kp, const SolveArgs& a, int cu_count, hipStream_t s) {
     if (a.n_tasks <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(a.queue, 0, sizeof(int), s);
+    hipError_t e = hipMemsetAsync(a.queue, 0, PC_QUEUE_INTS * sizeof(int), s);
     if (e != hipSuccess) return e;
     if (kp == 64) {
         constexpr int NG = CFK_PC64_NG, NS = 16 - CFK_PC64_NG;
@@ -2685,7 +2862,8 @@ GenericPlan generic_plan(int precision, int kp) {
     const int64_t elem = precision == 0 ? 4 : 8;
     const int64_t ntri = (int64_t)kp * (kp + 1) / 2;
     const int64_t tri_b = ((ntri + 1) & ~(int64_t)1) * elem;
-    const int64_t avail = 160 * 1024 - 1025 * elem;   // LDS minus the kernel's static RHS vector
+    // LDS minus the kernel's static vectors (RHS / solution; fp64: the refinement's residual and batch residuals)
+    const int64_t avail = 160 * 1024 - 1025 * elem - (precision == 0 ? 2 * 4 : (1024 + 64) * 8);
     const int64_t row_b = (int64_t)kp * elem;
     if (tri_b + 8 * row_b <= avail) {
         p.g_in_lds = true;

@@ -54,9 +54,16 @@ def test_cpu_share_honours_affinity_and_omp(monkeypatch):
     assert n3 == min(3, n) and "OMP_NUM_THREADS 3" in src3
 
 
-def test_bench_refuses_the_debug_library():
-    env = dict(os.environ, CFK_ALS_LIB=os.path.join(ROOT, "collaborative-filtering-kafka_amd", "build_debug",
-                                                    "libcfk_als.so"))
+@pytest.mark.parametrize("copy", [False, True])
+def test_bench_refuses_the_debug_library(tmp_path, copy):
+    """Refused by what the library exports (als_debug_knobs_compiled, debug build only), not by its path: a copy of
+    the diagnostics build under another name is refused too."""
+    import shutil
+    lib = os.path.join(ROOT, "collaborative-filtering-kafka_amd", "build_debug", "libcfk_als.so")
+    if copy:
+        shutil.copy(lib, tmp_path / "libcfk_als.so")
+        lib = str(tmp_path / "libcfk_als.so")
+    env = dict(os.environ, CFK_ALS_LIB=lib)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1"], env=env,
-                       capture_output=True, text=True, timeout=120)
-    assert r.returncode != 0 and "refused" in r.stderr
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "refused" in r.stderr, r.stderr[-2000:]

@@ -28,6 +28,7 @@ class OracleShardEngine:
         self.factors = [None, None]
         self.blocks = [None, None]
         self.layout = [(0, 0), (0, 0)]
+        self.chunks = [None, None]
 
     def set_row_layout(self, side, rows_per_chunk, chunk_stride):
         self.layout[side] = (int(rows_per_chunk), int(chunk_stride))
@@ -68,11 +69,11 @@ class OracleShardEngine:
         self.factors[side][self._rows(side, 0, len(out))] = torch.from_numpy(out)
 
     def set_chunks(self, side, bounds):
-        self.chunks = [(int(bounds[c]), int(bounds[c + 1])) for c in range(len(bounds) - 1)]
+        self.chunks[side] = [(int(bounds[c]), int(bounds[c + 1])) for c in range(len(bounds) - 1)]
 
     def solve_half_chunk(self, side, lam, c):
         rp, col, rat, off, n_opp = self.blocks[side]
-        lo, hi = self.chunks[c]
+        lo, hi = self.chunks[side][c]
         opp = self.factors[1 - side][:n_opp].numpy()
         sub = rp[lo:hi + 1] - rp[lo]
         s = self.oracle.Side(ids=np.arange(hi - lo), row_ptr=sub, col=col[rp[lo]:rp[hi]], ratings=rat[rp[lo]:rp[hi]])
@@ -86,7 +87,7 @@ class OracleShardEngine:
         return self.oracle.sq_error(s, self.factors[0][rows].numpy(), self.factors[1][:n_opp].numpy())
 
 
-def _worker(rank, world, port, path, out_dir, chunks=4):
+def _worker(rank, world, port, path, out_dir, chunks=4, movie_chunks=None):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -96,7 +97,8 @@ def _worker(rank, world, port, path, out_dir, chunks=4):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ds = cfk.Dataset.load_netflix(path)
-    app = cfk.ALSApp(4, 10, 0.05, 3, precision="f64", seed=42, rank=rank, world_size=world, overlap_chunks=chunks)
+    app = cfk.ALSApp(4, 10, 0.05, 3, precision="f64", seed=42, rank=rank, world_size=world, overlap_chunks=chunks,
+                     movie_chunks=movie_chunks)
     app.setup(ds, engine_factory=OracleShardEngine)
     app.run()
     U, M = app.factors()
@@ -113,12 +115,14 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,chunks", [(2, 1), (2, 4), (3, 3), (4, 7)])
-def test_sharded_driver_matches_single_process(cfk, oracle_mod, tiny_path, tmp_path, world, chunks):
+@pytest.mark.parametrize("world,chunks,movie_chunks", [(2, 1, None), (2, 4, None), (2, 4, 3), (3, 3, 2), (4, 7, None)])
+def test_sharded_driver_matches_single_process(cfk, oracle_mod, tiny_path, tmp_path, world, chunks, movie_chunks):
     """chunks > 1: the user half is solved in row-range chunks over chunk-major user slots; each chunk's
-    all-gather (async, one contiguous all_gather_into_tensor) overlaps the next chunk's solve."""
+    all-gather (async, one contiguous all_gather_into_tensor) overlaps the next chunk's solve. movie_chunks > 1:
+    the movie half the same way (chunk-major movie slots; automatic above ALSApp.MOVIE_CHUNK_BYTES)."""
     import torch.multiprocessing as mp
-    mp.spawn(_worker, args=(world, _free_port(), tiny_path, str(tmp_path), chunks), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), tiny_path, str(tmp_path), chunks, movie_chunks), nprocs=world,
+             join=True)
     m, u, r = oracle_mod.parse_netflix(tiny_path)
     b = oracle_mod.build_blocks(m, u, r)
     Uo, Mo = oracle_mod.run_als(b, 10, 0.05, 3, seed=42, precision="f64")

@@ -257,7 +257,7 @@ def _shard_data_worker(rank, world, port, out_dir, workload, restricted):
     else:
         ds = cfk.Dataset.synthetic_netflix(*shape, 5, nthreads=8)
     app = cfk.ALSApp(world, 64, LAM, 3, precision="f32", seed=9, device=0, rank=rank, world_size=world,
-                     overlap_chunks=2)
+                     overlap_chunks=2, movie_chunks=2)
     app.setup(ds, check_duplicates=False)
     app.run()
     U, M = app.factors()
@@ -268,7 +268,7 @@ def _shard_data_worker(rank, world, port, out_dir, workload, restricted):
 @pytest.mark.parametrize("workload", ["netflix", "powerlaw"])
 def test_two_ranks_on_shard_restricted_data(tmp_path, cfk, workload):
     """bench.py's multi-GPU data path at reduced size: each of 2 ranks (both on cuda:0, gloo carrying the
-    all-gathers, user half in 2 chunks) synthesizes ONLY its shard's ratings (als_dataset_synthetic_*_shard) and
+    all-gathers, both halves in 2 chunks: chunk-major movie and user slots) synthesizes ONLY its shard's ratings (als_dataset_synthetic_*_shard) and
     the factors and MSE are bitwise those of the same 2-rank run on the full dataset, and equal the 1-rank run's
     (same per-entity arithmetic; at this size every split row has the same chunking). Multi-GPU RCCL itself is
     measured only by the driver's 8-GPU run."""

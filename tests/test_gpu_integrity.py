@@ -153,3 +153,42 @@ def test_presplit_scale_extreme_factor_magnitudes(cfk, oracle_mod, scale):
             eng.close()
             assert np.all(np.isfinite(got))
             _check_vs_oracle(got, ref, ref32)
+
+
+@pytest.mark.parametrize("k", [64, 128])
+def test_presplit_range_guard(cfk, oracle_mod, monkeypatch, k):
+    """The fp16 pre-split uses one scale per table (split_exp): values far below the table's largest |x| lose
+    precision toward the fp16 subnormal floor. als_absmax also records the smallest nonzero row maximum; when the
+    table's rows span more than 2^16 (PRESPLIT_RANGE) the pre-split launch stands down and its guarded on-the-fly
+    launch (three-term bf16 split of the fp32 rows, an 8-bit exponent per value) solves the half.
+    - Row norms spanning 2^-24..1, both halves: within the reference's fp32 envelope, and bitwise the result of the
+      on-the-fly path (ALS_PRESPLIT=0), i.e. the guard fired.
+    - Columns of very unequal size (a mean-rating-sized column 0, the others ~1e-5 of it) keep every row's maximum in
+      range: the pre-split serves the half (not bitwise the on-the-fly result) and stays within the envelope."""
+    ds, b = _split_row_data(cfk, oracle_mod, seed=9)
+    rng = np.random.default_rng(k + 1)
+    for case in ("row_norms", "columns"):
+        for side, rows, opp in ((0, b.movie, b.user), (1, b.user, b.movie)):
+            n = len(opp.ids)
+            if case == "row_norms":
+                F = rng.random((n, k)) * 2.0 ** -rng.uniform(0, 24, size=(n, 1))
+                F[0] *= 1.0 / F[0].max()                # the extremes present: one row at 1 ...
+                F[1] *= 2.0 ** -24 / F[1].max()         # ... and one at 2^-24
+            else:
+                F = rng.random((n, k)) * 1e-5
+                F[:, 0] = 3.0 + rng.random(n)
+            F = F.astype(np.float32)
+            ref = oracle_mod.update_side(rows, F.astype(np.float64), LAM, "f64")
+            ref32 = oracle_mod.update_side(rows, F, LAM, "f32")
+            out = {}
+            for ps in ("1", "0"):
+                monkeypatch.setenv("ALS_PRESPLIT", ps)
+                eng = _engine(cfk, k, "f32", side, ds.shard_block(side), n, F)
+                assert eng.block_path(side)["presplit"] == (ps == "1")
+                eng.solve_half(side, LAM)
+                out[ps] = eng.read_factors(side)
+                eng.close()
+            monkeypatch.delenv("ALS_PRESPLIT")
+            assert np.all(np.isfinite(out["1"]))
+            _check_vs_oracle(out["1"], ref, ref32)
+            assert np.array_equal(out["1"], out["0"]) == (case == "row_norms"), (case, side)
