@@ -253,6 +253,15 @@ def main():
             dist.barrier()
 
     t_setup = time.perf_counter()
+    # a progress line on stderr every 30 s until the timed steps start (a multi-minute configs[4] synthesis and block
+    # build would otherwise print nothing for minutes)
+    import threading
+    setup_done = threading.Event()
+
+    def heartbeat():
+        while not setup_done.wait(30.0):
+            print(f"bench: rank {rank} setting up, {time.perf_counter() - t_setup:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
     nthreads = min(16, os.cpu_count() or 1)
     if solo:
         ds = cfk.Dataset.synthetic_shard(args.workload, users, movies, nnz_total, args.seed, args.shard_of,
@@ -276,6 +285,7 @@ def main():
                       dist.get_world_size() if world > 1 else 1)
     rccl_world = None if args.rehearse_one_gpu else exchange_world
 
+    setup_done.set()
     for _ in range(args.warmup):
         app.iteration()
     torch.cuda.synchronize()

@@ -622,6 +622,10 @@ __host__ __device__ constexpr int la_item_I(int C, int P, int t) {   // -1: the 
 #ifndef CFK_PS64_WAVES
 #define CFK_PS64_WAVES 4
 #endif
+// One-kernel pre-split launch at KP = 128: LDS-DMA two blocks ahead into two images (gram_presplit's DBUF)
+#ifndef CFK_PS128_DBUF
+#define CFK_PS128_DBUF 0
+#endif
 // One-kernel pre-split launch: the RHS by v_dot2_f32_f16 instead of 2 C MFMA tiles (gram_presplit's RHS mode)
 #ifndef CFK_PS_DOT2
 #define CFK_PS_DOT2 0
@@ -1150,9 +1154,12 @@ __device__ __forceinline__ void store_partial(const SolveArgs& a, const Task& tk
 // of its 8 entries times the rh and rm pairs (1) or the rh pairs alone when every rating is exact in fp16 (2),
 // per-lane partial sums reduced over the 4 lane rows at the end): 2 C MFMAs per block fewer, 8 C or 4 C VALU more.
 // The pipelined KP = 128 Gram role, whose wave has half the register file, needs both (108 MFMAs per block).
-template <int KP, bool NOE = false, int RHS = 0>
+// DBUF: the LDS-DMA two blocks ahead into two images (img, img2), so a block's DMA has two blocks' MFMAs to land
+// under instead of one (the one-wave-per-SIMD KP = 128 launch, where no other wave covers the wait).
+template <int KP, bool NOE = false, int RHS = 0, bool DBUF = false>
 __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk, MfmaAcc<KP / 16>& acc,
-                                              f32x4 (&E)[KP / 16], unsigned char* img, float* buf, int lane) {
+                                              f32x4 (&E)[KP / 16], unsigned char* img, float* buf, int lane,
+                                              unsigned char* img2 = nullptr) {
     constexpr int C = KP / 16;
     using Acc = MfmaAcc<C>;
     constexpr int B = BLOCK_SUBSTEPS;
@@ -1251,7 +1258,7 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
         tpl[x] = tbase + (x / NH) * 2 * KP + (x % NH) * 128;
         asm volatile("" : "+s"(tpl[x]));
     }
-    auto issue = [&](const i32x4& cv) {
+    auto issue_to = [&](const i32x4& cv, unsigned char* im) {
         static_for<0, 4>([&](auto M_) {
             constexpr int m = decltype(M_)::value;
             // 24-bit multiply: pre-split tables are host-checked < 2^24 rows and < 4 GiB
@@ -1259,29 +1266,76 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
             static_for<0, NPL * NH>([&](auto X_) {
                 constexpr int x = decltype(X_)::value;   // plane x / NH, half x % NH
                 __builtin_amdgcn_global_load_lds((const void*)(tpl[x] + vo),
-                                                 (lds_void*)(img + (x * 4 + m) * 1024), 16, 0, 0);
+                                                 (lds_void*)(im + (x * 4 + m) * 1024), 16, 0, 0);
             });
         });
     };
-    auto read1 = [&](auto PL_, auto B_) {
+    auto issue = [&](const i32x4& cv) { issue_to(cv, img); };
+    auto read1 = [&](auto PL_, auto B_, unsigned char* im) {
         constexpr int pl = decltype(PL_)::value, b = decltype(B_)::value;
         u32x4 P;
         static_for<0, 2>([&](auto H_) {
             constexpr int h = decltype(H_)::value;
             const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_s16x4*)(img + rd[b & 3] + ((pl * NH + (b >> 2)) * 4 + h) * 1024));
+                (lds_s16x4*)(im + rd[b & 3] + ((pl * NH + (b >> 2)) * 4 + h) * 1024));
             const u32x2 w = __builtin_bit_cast(u32x2, v);
             P[2 * h] = w[0];
             P[2 * h + 1] = w[1];
         });
         return P;
     };
-    auto read = [&](u32x4 (&P)[NPL][C]) {
+    auto read_from = [&](u32x4 (&P)[NPL][C], unsigned char* im) {
         static_for<0, NPL>([&](auto PL_) {
-            static_for<0, C>([&](auto B_) { P[decltype(PL_)::value][decltype(B_)::value] = read1(PL_, B_); });
+            static_for<0, C>([&](auto B_) { P[decltype(PL_)::value][decltype(B_)::value] = read1(PL_, B_, im); });
         });
     };
-    if (nblk > 0) {
+    auto read = [&](u32x4 (&P)[NPL][C]) { read_from(P, img); };
+    if constexpr (DBUF) {
+        static_assert(RHS == 0, "double-buffered pre-split Gram: RHS MFMA tiles");
+        if (nblk > 0) {
+            const int lastb = nblk - 1;
+            const i32x4* cp = (const i32x4*)(a.col_ps + tk.begin) + r8;   // + 8 per block
+            const u32x4* rp = (const u32x4*)(a.rat_pk + (j >= 8 ? a.rat_lo_off : 0) + (tk.begin >> 1)) + g;
+            // Vector-memory ops per block, in order: its image's DMA (2 C instructions), the column indices of the
+            // block two ahead, the ratings of this block. Steady state at block b's wait: after DMA(b) come cv(b+2),
+            // R(b), then block b+1's DMA, cv(b+3), R(b+1) -- so vmcnt(2 C + 2) leaves exactly block b+1's ops in
+            // flight (DMA(b), cv(b+2) and R(b) done). Past the end the DMAs repeat the last block (same counts).
+            constexpr int AHEAD = NPL * NH * 4 + 2;
+            i32x4 cv0 = cp[0], cv1 = cp[8 * min(1, lastb)];
+            issue_to(cv0, img);
+            cv0 = cp[8 * min(2, lastb)];
+            u32x4 R0 = rp[0];
+            issue_to(cv1, img2);
+            cv1 = cp[8 * min(3, lastb)];
+            u32x4 R1 = rp[4 * min(1, lastb)];
+            static_assert(AHEAD == 18, "DBUF vmcnt below assumes 16 DMA instructions per block (KP = 128)");
+            for (int b = 0; b < nblk; b += 2) {
+                u32x4 P[NPL][C];
+                asm volatile("s_waitcnt vmcnt(18)" ::: "memory");   // DMA(b), cv(b+2), R(b) (tests/test_isa_guard.py)
+                read_from(P, img);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // operands in registers: the image is free
+                const u32x4 Ra = R0;
+                issue_to(cv0, img);                                  // DMA(b+2)
+                cv0 = cp[8 * min(b + 4, lastb)];
+                R0 = rp[4 * min(b + 2, lastb)];
+                __builtin_amdgcn_sched_barrier(0);
+                mfma_block(P, Ra, Ra);
+                __builtin_amdgcn_sched_barrier(0);
+                if (b + 1 > lastb) break;                             // wave-uniform
+                asm volatile("s_waitcnt vmcnt(18)" ::: "memory");   // DMA(b+1), cv(b+3), R(b+1)
+                read_from(P, img2);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const u32x4 Rb = R1;
+                issue_to(cv1, img2);                                 // DMA(b+3)
+                cv1 = cp[8 * min(b + 5, lastb)];
+                R1 = rp[4 * min(b + 3, lastb)];
+                __builtin_amdgcn_sched_barrier(0);
+                mfma_block(P, Rb, Rb);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMAs issued past the last block have landed
+        }
+    } else if (nblk > 0) {
         const int lastb = nblk - 1;
         const i32x4* cp = (const i32x4*)(a.col_ps + tk.begin) + r8;          // + 8 per block
         // rating pairs of the lane's column half: rh (columns 0-7) or rm (columns 8-15); dot2 RHS: rh, rm in Rmn
@@ -1354,7 +1408,7 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
 // GRIDLOOP: a grid-stride loop over the tasks (the range guard's fallback launch, whose grid is capped: when the
 // pre-split serves the half, as it nearly always does, its waves exit without a full-size grid's dispatch cost).
 template <int KP, int MINW, bool SPLIT, bool PRESPLIT = false, bool REDUCE = false, bool NOE = false, int RHS = 0,
-          bool GRIDLOOP = false>
+          bool GRIDLOOP = false, bool DBUF = false>
 __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(SolveArgs a) {
     constexpr int C = KP / 16;
     constexpr int NW = mfma_waves<KP>();
@@ -1371,6 +1425,9 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
     constexpr int STAGE = (PRESPLIT && !REDUCE) ? 2 * C * 1024 : 16;
     __shared__ __attribute__((aligned(1024))) unsigned char stage_lds[NW][STAGE];
     (void)stage_lds;
+    // DBUF: the second image per wave, a separate LDS object
+    __shared__ __attribute__((aligned(1024))) unsigned char stage_lds2[NW][DBUF ? STAGE : 16];
+    (void)stage_lds2;
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // the table-range guard (presplit_ok): a pre-split launch serves the half only in range, its guarded on-the-fly
@@ -1464,7 +1521,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                 for (int c = 0; c < C; ++c) acc.rhs[c] += r * y[c];
             };
             if constexpr (PRESPLIT) {
-                gram_presplit<KP, NOE, RHS>(a, tk, acc, E, stage_lds[uni(wave)], buf, lane);
+                gram_presplit<KP, NOE, RHS, DBUF>(a, tk, acc, E, stage_lds[uni(wave)], buf, lane, stage_lds2[uni(wave)]);
             } else if constexpr (SPLIT) {
                 // Split-bf16 Gram: one v_mfma_f32_16x16x32_bf16 consumes a whole 32-entry block. Lane (g, j)
                 // holds A[i = j][k = 8g + t] = y_t[C*j + b] (its own gathered piece, component b, entry t of its
@@ -2661,6 +2718,10 @@ hipError_t launch_solve_t(const SolveArgs& a, hipStream_t s, bool reduce) {
                 als_solve_mfma<KP, MINW, SPLIT, PRESPLIT, false, false, 2><<<grid, 64 * nw, dyn, s>>>(a);
             else
                 als_solve_mfma<KP, MINW, SPLIT, PRESPLIT, false, false, 1><<<grid, 64 * nw, dyn, s>>>(a);
+        } else if constexpr (PRESPLIT && KP == 128 && CFK_PS128_DBUF) {
+            // the second image's column / rating registers: the diagonal tiles take hh + hm + mh (NOE) so the
+            // Gram keeps no register copies inside its MFMA groups (tests/test_isa_guard.py)
+            als_solve_mfma<KP, MINW, SPLIT, PRESPLIT, false, true, 0, false, true><<<grid, 64 * nw, dyn, s>>>(a);
         } else {
             als_solve_mfma<KP, MINW, SPLIT, PRESPLIT><<<grid, 64 * nw, dyn, s>>>(a);
         }

@@ -92,6 +92,9 @@ def _writes(op, ops):
     return set()
 
 
+MFMA_SAFE_WS = 64
+
+
 def test_every_split_gram_mfma_is_drained_before_its_operands_change(kernels):
     checked, violations = 0, []
     for name, ins in _solve_kernels(kernels).items():
@@ -109,12 +112,20 @@ def test_every_split_gram_mfma_is_drained_before_its_operands_change(kernels):
                     break
                 if op2.startswith(("s_branch", "s_cbranch", "s_setpc", "s_endpgm")):
                     break
-                ws += int(ops2[0], 0) + 1 if op2 == "s_nop" else 1
+                # wait states: s_nop N = N + 1; a later MFMA holds issue >= 8 cycles (a 16x16x32 one 16); others >= 1
+                ws += int(ops2[0], 0) + 1 if op2 == "s_nop" else 8 if op2.startswith("v_mfma") else 1
                 if op2.startswith("v_mfma"):
                     continue
                 w = _writes(op2, ops2)
                 if w & srcs:
-                    violations.append((name, i, op2, " ".join(ops2[:2]), ws))
+                    # a source rewritten inside the group: a hazard only while the MFMA may still be reading it --
+                    # within MFMA_SAFE_WS wait states (each counted instruction takes >= 1 cycle, a 16x16x32 MFMA
+                    # reads its sources in its first 16). The register allocator's AGPR copies deep inside a long
+                    # KP = 128 group (hundreds of wait states on) are not.
+                    if ws < MFMA_SAFE_WS:
+                        violations.append((name, i, op2, " ".join(ops2[:2]), ws))
+                    else:
+                        drained = True   # long done reading
                     break
             if not drained and not (violations and violations[-1][1] == i):
                 violations.append((name, i, "no MFMA_DRAIN before a branch / the end", ""))
@@ -142,3 +153,26 @@ def test_lds_dma_image_waited_before_transposed_reads(kernels):
                     bad.append((name, i, last_dma))
     assert checked >= 32, checked
     assert not bad, bad[:8]
+
+
+def test_double_buffered_dma_counts_match_the_vmcnt(kernels):
+    """The double-buffered pre-split Gram (gram_presplit DBUF, KP = 128) waits `s_waitcnt vmcnt(18)` before reading a
+    block's image: correct only if every block issues exactly 18 vector-memory instructions (its 16 LDS-DMA plus the
+    column-index and rating loads) between consecutive waits, so that the 18 still outstanding are the NEXT block's.
+    Checked on the code object: between two vmcnt(18) waits inside the loop, 18 VMEM ops, 16 of them LDS-DMA."""
+    found = 0
+    for name, ins in _solve_kernels(kernels).items():
+        waits = [i for i, (op, ops) in enumerate(ins) if op == "s_waitcnt" and "vmcnt(18)" in " ".join(ops)]
+        if len(waits) < 2 or not any(op == "global_load_lds_dwordx4" for op, _ in ins):
+            continue   # (compiler-placed vmcnt(18) waits elsewhere are not this scheme)
+        found += 1
+        for a in waits:   # from each wait to the next branch (the loop's break test / back edge) or wait
+            seg = []
+            for op, _ in ins[a + 1:]:
+                if op.startswith("s_cbranch") or op == "s_endpgm":
+                    break
+                seg.append(op)
+            vmem = [op for op in seg if op.startswith(("global_load", "buffer_load", "global_atomic"))]
+            assert len(vmem) == 18 and sum(op == "global_load_lds_dwordx4" for op in vmem) == 16, (name, a, len(vmem))
+    if not found:
+        pytest.skip("no double-buffered pre-split kernel in this build (CFK_PS128_DBUF=0)")
