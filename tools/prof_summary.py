@@ -29,10 +29,23 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def is_reduce(name):
+def mfma_args(name):
+    """template arguments of an als_solve_mfma instantiation: <KP, MINW, SPLIT, PRESPLIT, REDUCE, NOE, RHS, GRIDLOOP,
+    DBUF> (als_kernels.hip)"""
     if "als_solve_mfma<" not in name:
-        return False
-    return name.split("als_solve_mfma<", 1)[1].split(">")[0].split(",")[-1].strip() == "true"
+        return None
+    return [a.strip() for a in name.split("als_solve_mfma<", 1)[1].split(">")[0].split(",")]
+
+
+def is_reduce(name):
+    a = mfma_args(name)
+    return bool(a) and len(a) > 4 and a[4] == "true"
+
+
+def is_fallback(name):
+    """the pre-split range guard's grid-stride fallback launch (waves exit at once while the table is in range)"""
+    a = mfma_args(name)
+    return bool(a) and len(a) > 7 and a[7] == "true"
 
 
 def role_of(name, grid, grids):
@@ -42,6 +55,8 @@ def role_of(name, grid, grids):
         return "dual"
     if is_reduce(name):
         return "reduce"
+    if is_fallback(name):
+        return "fallback"
     big = sorted(grids, reverse=True)
     if grid == big[0]:
         return "user"
@@ -68,7 +83,8 @@ def main(tag, name):
     if st:
         shutil.copy(st[0], os.path.join(dst, "kernel_stats.csv"))
     grid = lambda r: int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)
-    grids = {grid(r) for r in tr if "als_solve_mfma" in r["Kernel_Name"] and not is_reduce(r["Kernel_Name"])}
+    grids = {grid(r) for r in tr if "als_solve_mfma" in r["Kernel_Name"] and not is_reduce(r["Kernel_Name"])
+             and not is_fallback(r["Kernel_Name"])}
     dur = defaultdict(list)
     for r in tr:
         role = role_of(r["Kernel_Name"], grid(r), grids)
@@ -80,7 +96,8 @@ def main(tag, name):
     # --- PMC passes ---
     def per_role(pattern):
         rows = load_rows(pattern)
-        g = {int(r["Grid_Size"]) for r in rows if "als_solve_mfma" in r["Kernel_Name"] and not is_reduce(r["Kernel_Name"])}
+        g = {int(r["Grid_Size"]) for r in rows if "als_solve_mfma" in r["Kernel_Name"] and not is_reduce(r["Kernel_Name"])
+             and not is_fallback(r["Kernel_Name"])}
         acc = defaultdict(lambda: defaultdict(list))
         disp = defaultdict(lambda: defaultdict(float))
         for r in rows:
