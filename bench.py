@@ -172,10 +172,18 @@ def build_record():
     return rec
 
 
-def load_counters(k, nnz, lib_sha):
-    """Per-launch rocprofv3 counters at (k, nnz) of THIS library build (profiles/counters_k<k>.json, stamped with
+def counters_path(k, workload="netflix", shard_of=0):
+    """profiles/counters_k<k>.json for the metric's workload on the whole dataset, else
+    counters_k<k>_<workload>[_shard<G>].json (tools/prof_summary.py counters_name writes the same names)"""
+    if workload == "netflix" and not shard_of:
+        return os.path.join(ROOT, "profiles", f"counters_k{k}.json")
+    return os.path.join(ROOT, "profiles", f"counters_k{k}_{workload}" + (f"_shard{shard_of}" if shard_of else "") + ".json")
+
+
+def load_counters(k, nnz, lib_sha, workload="netflix", shard_of=0):
+    """Per-launch rocprofv3 counters at (k, nnz) of THIS library build (profiles/counters_k<k>*.json, stamped with
     the profiled library's sha256 by tools/prof_summary.py): (counters, None) or (None, why they were dropped)."""
-    path = os.path.join(ROOT, "profiles", f"counters_k{k}.json")
+    path = counters_path(k, workload, shard_of)
     try:
         c = json.load(open(path))
     except (OSError, ValueError):
@@ -318,7 +326,8 @@ def main():
     if rank == 0:
         build = build_record()
         info = {"movie": app.info[0], "user": app.info[1]}
-        ctr, ctr_why = load_counters(args.k, nnz_total, build["lib_sha256"]) if world == 1 else (None, "N > 1")
+        ctr, ctr_why = (load_counters(args.k, nnz_total, build["lib_sha256"], args.workload,
+                                      args.shard_of if solo else 0) if world == 1 else (None, "N > 1"))
         kp = eng.kp
         per = {}
         for si, side in enumerate(("movie", "user")):

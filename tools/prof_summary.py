@@ -65,6 +65,16 @@ def role_of(name, grid, grids):
     return "other"
 
 
+def counters_name(k, cfg):
+    """profiles/ file of a profiled configuration (bench.py counters_path reads the same name): counters_k<k>.json for
+    the metric's workload on the whole dataset, counters_k<k>_<workload>[_shard<G>].json otherwise"""
+    wl = cfg.get("workload_name", "netflix")
+    shard = cfg.get("shard_of")
+    if wl == "netflix" and not shard:
+        return f"counters_k{k}.json"
+    return f"counters_k{k}_{wl}" + (f"_shard{shard}" if shard else "") + ".json"
+
+
 def load_rows(pattern):
     rows = []
     for f in glob.glob(pattern, recursive=True):
@@ -183,7 +193,7 @@ def main(tag, name):
                "note": "per launch; hbm_bytes = FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> B (Infinity-Cache "
                        "hits are counted by these counters); *_frac over 1024 SIMDs x the launch's GPU cycles "
                        "(GRBM_GUI_ACTIVE / 8 XCDs)"},
-              open(os.path.join(ROOT, "profiles", f"counters_k{k}.json"), "w"), indent=1)
+              open(os.path.join(ROOT, "profiles", counters_name(k, cfg)), "w"), indent=1)
     print(json.dumps({k: out[k] for k in ("trace", "traffic")}, indent=1))
 
 
