@@ -455,7 +455,10 @@ def main():
                        "movie_chunks": app.info[0]["n_chunks"] if world > 1 else None,
                        "rehearsal_gloo_one_gpu": bool(args.rehearse_one_gpu),
                        "shard_of": args.shard_of if solo else None, "shard_rank": args.shard_rank if solo else None,
-                       "shard_ratings": shard_nnz if solo else None},
+                       "shard_ratings": shard_nnz if solo else None,
+                       # main launches per half-iteration (one per slot chunk; tools/prof_summary.py groups the
+                       # kernel trace by these)
+                       "launches_per_half": {"movie": app.info[0]["n_chunks"], "user": app.info[1]["n_chunks"]}},
             "solves_per_s": ((info["movie"]["n_rows"] + info["user"]["n_rows"]) if solo else (nm + nu)) * K / elapsed,
             "projected_job_ratings_per_s_compute_only": value * args.shard_of if solo else None,
             "mse_after": mse,

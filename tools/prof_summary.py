@@ -16,7 +16,7 @@ phase = whole launch minus Gram-only counters (its share of the launch's cycles,
 Sides: the main solve kernel dispatch with the largest grid is the user half (480,189 tasks), the next the movie
 half (FULL + PARTIAL tasks); the REDUCE kernel instantiation is recognised by its last template argument.
 
-  python tools/prof_summary.py <tag> <profiles subdir>
+  python tools/prof_summary.py <tag> <profiles subdir> [<movie launches per half> <user launches per half>]
 """
 import csv
 import glob
@@ -65,6 +65,25 @@ def role_of(name, grid, grids):
     return "other"
 
 
+def half_groups(rows, per_half):
+    """{Dispatch_Id: (role, half index)} for the main launches (als_solve_mfma, neither REDUCE nor the guard's
+    fallback) of the rows, in dispatch order: every iteration runs per_half["movie"] movie-half launches (one per slot
+    chunk), then per_half["user"] user-half launches (bench.py config launches_per_half). None when the launch count
+    does not fit that pattern (the caller then tells the halves apart by grid size)."""
+    if not per_half:
+        return None
+    lm, lu = int(per_half["movie"]), int(per_half["user"])
+    ids = sorted({int(r["Dispatch_Id"]) for r in rows if "als_solve_mfma" in r["Kernel_Name"]
+                  and not is_reduce(r["Kernel_Name"]) and not is_fallback(r["Kernel_Name"])})
+    if not ids or len(ids) % (lm + lu):
+        return None
+    out = {}
+    for i, d in enumerate(ids):
+        pos = i % (lm + lu)
+        out[d] = ("movie" if pos < lm else "user", i // (lm + lu))
+    return out
+
+
 def counters_name(k, cfg):
     """profiles/ file of a profiled configuration (bench.py counters_path reads the same name): counters_k<k>.json for
     the metric's workload on the whole dataset, counters_k<k>_<workload>[_shard<G>].json otherwise"""
@@ -82,7 +101,7 @@ def load_rows(pattern):
     return rows
 
 
-def main(tag, name):
+def main(tag, name, launches=None):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles", name)
     os.makedirs(dst, exist_ok=True)
@@ -92,29 +111,52 @@ def main(tag, name):
     st = glob.glob(f"{src}/trace/**/*kernel_stats.csv", recursive=True)
     if st:
         shutil.copy(st[0], os.path.join(dst, "kernel_stats.csv"))
+    bl = os.path.join(src, "bench.json")
+    cfg0 = {}
+    if os.path.exists(bl):
+        ls = [l for l in open(bl) if l.startswith("{")]
+        cfg0 = json.loads(ls[-1]).get("config", {}) if ls else {}
+    per_half = cfg0.get("launches_per_half") or launches
+
     grid = lambda r: int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)
     grids = {grid(r) for r in tr if "als_solve_mfma" in r["Kernel_Name"] and not is_reduce(r["Kernel_Name"])
              and not is_fallback(r["Kernel_Name"])}
+    groups = half_groups(tr, per_half)
     dur = defaultdict(list)
+    half_ms = defaultdict(lambda: defaultdict(float))   # one half = the sum of its chunk launches
     for r in tr:
+        ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        g = groups.get(int(r["Dispatch_Id"])) if groups else None
+        if g:
+            half_ms[g[0]][g[1]] += ms
+            continue
         role = role_of(r["Kernel_Name"], grid(r), grids)
         if role:
-            dur[role].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+            dur[role].append(ms)
+    for role, h in half_ms.items():
+        dur[role] = [h[i] for i in sorted(h)]
     out["trace"] = {k: {"calls": len(v), "avg_ms": sum(v) / len(v), "min_ms": min(v), "max_ms": max(v),
                         "avg_ms_without_first": sum(v[1:]) / max(1, len(v) - 1)} for k, v in dur.items()}
-    json.dump({"source": f"prof_{tag}/trace", "launches": out["trace"]}, open(os.path.join(dst, "main_launch_summary.json"), "w"), indent=1)
+    json.dump({"source": f"prof_{tag}/trace", "launches_per_half": per_half, "launches": out["trace"],
+               "note": "movie / user: per half-iteration, the sum of its main launches (one per slot chunk)"},
+              open(os.path.join(dst, "main_launch_summary.json"), "w"), indent=1)
     # --- PMC passes ---
     def per_role(pattern):
         rows = load_rows(pattern)
         g = {int(r["Grid_Size"]) for r in rows if "als_solve_mfma" in r["Kernel_Name"] and not is_reduce(r["Kernel_Name"])
              and not is_fallback(r["Kernel_Name"])}
+        hg = half_groups(rows, per_half)
         acc = defaultdict(lambda: defaultdict(list))
         disp = defaultdict(lambda: defaultdict(float))
         for r in rows:
+            h = hg.get(int(r["Dispatch_Id"])) if hg else None
+            if h:   # a half's chunk launches summed: counters per half-iteration, like the bench's launch time
+                disp[(h[0], "half", h[1])][r["Counter_Name"]] += float(r["Counter_Value"])
+                continue
             role = role_of(r["Kernel_Name"], int(r["Grid_Size"]), g)
             if role:
                 disp[(role, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
-        for (role, _), cnt in disp.items():
+        for (role, *_), cnt in disp.items():
             for c, v in cnt.items():
                 acc[role][c].append(v)
         return {role: {c: sum(v) / len(v) for c, v in cs.items()} for role, cs in acc.items()}
@@ -198,4 +240,6 @@ def main(tag, name):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    # optional: movie / user launches per half for a bench line that predates config.launches_per_half
+    main(sys.argv[1], sys.argv[2],
+         {"movie": int(sys.argv[3]), "user": int(sys.argv[4])} if len(sys.argv) > 4 else None)
