@@ -543,6 +543,30 @@ __device__ __forceinline__ float row_sum_to_last(float v) {
 // a[i][p] + a[i][p] (d - 1)(-1/d) = a[i][p] / d. That FMA is accurate to a few ulp only while d <= 1,
 // which the caller guarantees by Jacobi-scaling the system to a unit diagonal (every later pivot is a
 // Schur-complement diagonal of a unit-diagonal SPD matrix, so it stays in (0, 1]).
+// CFK_SWEEP_DPPFMA: the four row broadcasts fused into the FMAs (v_fmac_f32_dpp row_newbcast, one instruction per
+// register instead of a v_mov_b32_dpp + v_fmac_f32 pair; k = 64 / 128 user half -3 %, profiles/r05e/e18_*.log).
+// A DPP read of a VGPR needs 2 wait states after a VALU write of it, and the compiler's hazard recognizer does not
+// see VALU writes inside inline asm: the block waits 2 states before its first DPP read (the previous step's writes)
+// and after its last write (a compiler-placed DPP or lane op reading the results next).
+#ifndef CFK_SWEEP_DPPFMA
+#define CFK_SWEEP_DPPFMA 1
+#endif
+template <int L>
+__device__ __forceinline__ void fmac_rowbcast4(f32x4& a, float t) {
+    float a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
+    asm("s_nop 1\n\t"
+        "v_fmac_f32_dpp %0, %0, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, %1, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %2, %2, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %3, %3, %4 row_newbcast:%5 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1"
+        : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)
+        : "v"(t), "i"(L));
+    a[0] = a0;
+    a[1] = a1;
+    a[2] = a2;
+    a[3] = a3;
+}
 template <bool SWAP, int p>
 __device__ __forceinline__ void sweep_step(f32x4& a, int lane, float& nrd_min) {
     constexpr int pg = p >> 2, pr = p & 3;
@@ -551,11 +575,15 @@ __device__ __forceinline__ void sweep_step(f32x4& a, int lane, float& nrd_min) {
     const bool piv = lane == 16 * pg + p;   // 16 lane masks, CSE-d across the 4 diagonal tiles (SGPRs)
     a[pr] = piv ? a[pr] - 1.f : a[pr];
     const float t = (SWAP ? col_bcast_swap<pg>(a[pr]) : col_bcast<pg>(a[pr])) * nrd;   // a[p][c] (d - 1 at c = p) * (-1/d)
-    f32x4 cp;
+    if constexpr (CFK_SWEEP_DPPFMA) {
+        fmac_rowbcast4<p>(a, t);   // a[4g + r][c] += a[4g + r][p] t[c]
+    } else {
+        f32x4 cp;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) cp[r] = row_lane_bcast<p>(a[r]);   // a[4g + r][p] (d - 1 at row p)
+        for (int r = 0; r < 4; ++r) cp[r] = row_lane_bcast<p>(a[r]);   // a[4g + r][p] (d - 1 at row p)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) a[r] += cp[r] * t;
+        for (int r = 0; r < 4; ++r) a[r] += cp[r] * t;
+    }
     a[pr] = piv ? nrd : a[pr];
 }
 template <bool SWAP>
