@@ -164,11 +164,18 @@ def build_record():
     import __graft_entry__
     from cfk_amd import _lib
     path = os.path.realpath(_lib.LIB_PATH)
-    rec = {"lib_path": os.path.relpath(path, ROOT), "lib_sha256": __graft_entry__.sha256_file(path)}
+    rec = {"lib_path": os.path.relpath(path, ROOT), "lib_sha256": __graft_entry__.sha256_file(path),
+           "device_code_sha256": __graft_entry__.device_code_sha256(path)}
     info = __graft_entry__.build_info("product")
+    tree = __graft_entry__.source_digest()
     if info and info.get("lib_sha256") == rec["lib_sha256"]:
         rec["source_sha256"] = info.get("source_sha256")
-        rec["source_matches_tree"] = info.get("source_sha256") == __graft_entry__.source_digest()
+        rec["source_matches_tree"] = info.get("source_sha256") == tree
+    # the digest compiled into the binary itself (als_build_source_sha256): the source <-> binary link without the
+    # build's own BUILD_INFO.json
+    embedded = _lib.lib().als_build_source_sha256().decode() or None
+    rec["binary_source_sha256"] = embedded
+    rec["binary_matches_tree"] = embedded == tree if embedded else None
     return rec
 
 
@@ -180,9 +187,11 @@ def counters_path(k, workload="netflix", shard_of=0):
     return os.path.join(ROOT, "profiles", f"counters_k{k}_{workload}" + (f"_shard{shard_of}" if shard_of else "") + ".json")
 
 
-def load_counters(k, nnz, lib_sha, workload="netflix", shard_of=0):
-    """Per-launch rocprofv3 counters at (k, nnz) of THIS library build (profiles/counters_k<k>*.json, stamped with
-    the profiled library's sha256 by tools/prof_summary.py): (counters, None) or (None, why they were dropped)."""
+def load_counters(k, nnz, lib_sha, workload="netflix", shard_of=0, dev_sha=None):
+    """Per-launch rocprofv3 counters at (k, nnz) of THIS library's kernels (profiles/counters_k<k>*.json, stamped by
+    tools/prof_summary.py with the profiled library's sha256 and the sha256 of its device code): valid when either
+    matches (a host-code-only rebuild keeps the kernels and so the counters). (counters, None) or (None, why they
+    were dropped)."""
     path = counters_path(k, workload, shard_of)
     try:
         c = json.load(open(path))
@@ -190,10 +199,12 @@ def load_counters(k, nnz, lib_sha, workload="netflix", shard_of=0):
         return None, f"no {os.path.relpath(path, ROOT)}"
     if c.get("k") != k or c.get("nnz") != nnz:
         return None, f"{os.path.relpath(path, ROOT)} was profiled at k={c.get('k')} nnz={c.get('nnz')}"
-    if c.get("lib_sha256") != lib_sha:
-        return None, (f"stale: {c.get('source')} profiled library {str(c.get('lib_sha256'))[:12]} != this build "
-                      f"{lib_sha[:12]}")
-    return c, None
+    if c.get("lib_sha256") == lib_sha:
+        return dict(c, matched_by="lib_sha256"), None
+    if dev_sha and c.get("device_code_sha256") == dev_sha:
+        return dict(c, matched_by="device_code_sha256"), None
+    return None, (f"stale: {c.get('source')} profiled library {str(c.get('lib_sha256'))[:12]} != this build "
+                  f"{lib_sha[:12]} (device code {str(c.get('device_code_sha256'))[:12]} != {str(dev_sha)[:12]})")
 
 
 def main():
@@ -327,7 +338,8 @@ def main():
         build = build_record()
         info = {"movie": app.info[0], "user": app.info[1]}
         ctr, ctr_why = (load_counters(args.k, nnz_total, build["lib_sha256"], args.workload,
-                                      args.shard_of if solo else 0) if world == 1 else (None, "N > 1"))
+                                      args.shard_of if solo else 0, build["device_code_sha256"])
+                        if world == 1 else (None, "N > 1"))
         kp = eng.kp
         per = {}
         for si, side in enumerate(("movie", "user")):

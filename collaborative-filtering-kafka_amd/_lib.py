@@ -56,6 +56,7 @@ _ppv = ctypes.POINTER(ctypes.c_void_p)
 SIGNATURES = [
     ("als_abi_version", _i, []),
     ("als_last_error", ctypes.c_char_p, []),
+    ("als_build_source_sha256", ctypes.c_char_p, []),
     ("als_device_count", _i, [ctypes.POINTER(ctypes.c_int)]),
     ("als_engine_create", _i, [_i, _i, _i, _ppv]),
     ("als_engine_destroy", _i, [_vp]),

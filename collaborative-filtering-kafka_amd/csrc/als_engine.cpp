@@ -237,6 +237,16 @@ int als_device_count(int* n) {
 }
 const char* als_last_error(void) { return g_last_error.c_str(); }
 
+#define CFK_STR2(x) #x
+#define CFK_STR(x) CFK_STR2(x)
+const char* als_build_source_sha256(void) {
+#ifdef CFK_SOURCE_SHA256
+    return &CFK_STR(CFK_SOURCE_SHA256)[1];   // "h<digest>": an identifier token, the h dropped
+#else
+    return "";
+#endif
+}
+
 int als_engine_create(int device, int num_features, int precision, als_engine** out) {
     if (!out) return fail(ALS_ERR_INVALID_ARGUMENT, "out is NULL");
     *out = nullptr;

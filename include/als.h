@@ -56,6 +56,9 @@ typedef struct als_engine als_engine;
 /* ---- version / errors --------------------------------------------------------------------------- */
 int         als_abi_version(void);
 const char* als_last_error(void);
+/* sha256 of the sources (csrc/, include/) the library was compiled from, as stamped by the build
+ * (__graft_entry__.build); "" for an unstamped developer build. */
+const char* als_build_source_sha256(void);
 int         als_device_count(int* n);
 
 /* ---- engine lifetime ---------------------------------------------------------------------------- */

@@ -30,6 +30,34 @@ def test_counters_used_for_the_profiled_library_only(tmp_path, monkeypatch):
     assert c is None and why.startswith("stale:") and "aaaaaaaaaaaa" in why and "bbbbbbbbbbbb" in why
 
 
+def test_counters_follow_the_device_code_across_host_only_rebuilds(tmp_path, monkeypatch):
+    """counters stamped with the profiled library's device-code hash stay valid for a library whose host code
+    changed but whose .hip_fatbin (the kernels) did not; a different device code drops them"""
+    _write_counters(tmp_path, monkeypatch, device_code_sha256="d" * 64)
+    c, why = bench.load_counters(64, 1000, "b" * 64, dev_sha="d" * 64)
+    assert c is not None and why is None and c["matched_by"] == "device_code_sha256"
+    c, why = bench.load_counters(64, 1000, "b" * 64, dev_sha="e" * 64)
+    assert c is None and why.startswith("stale:")
+
+
+def test_device_code_hash_reads_the_fatbin_section(cfk):
+    """__graft_entry__.device_code_sha256 = sha256 of the library's .hip_fatbin section, as llvm-objcopy dumps it"""
+    import subprocess
+    import hashlib
+    import __graft_entry__
+    from cfk_amd import _lib
+    path = os.path.realpath(_lib.LIB_PATH)
+    out = os.path.join(os.path.dirname(path), "fatbin_test.bin")
+    try:
+        subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objcopy", "--dump-section", f".hip_fatbin={out}", path,
+                        out + ".so"], check=True)
+        assert __graft_entry__.device_code_sha256(path) == hashlib.sha256(open(out, "rb").read()).hexdigest()
+    finally:
+        for f in (out, out + ".so"):
+            if os.path.exists(f):
+                os.remove(f)
+
+
 def test_counters_of_another_workload_are_dropped(tmp_path, monkeypatch):
     _write_counters(tmp_path, monkeypatch)
     assert bench.load_counters(64, 2000, "a" * 64)[0] is None

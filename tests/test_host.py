@@ -33,6 +33,18 @@ def test_library_exports_every_declared_symbol(cfk):
     assert L.als_abi_version() == 3
 
 
+def test_library_carries_its_source_digest(cfk):
+    """A library built by __graft_entry__.build() has the digest of the sources it was compiled from inside the
+    binary (als_build_source_sha256), equal to its BUILD_INFO.json stamp; an unstamped developer build returns ""."""
+    import __graft_entry__
+    from cfk_amd import _lib
+    embedded = _lib.lib().als_build_source_sha256().decode()
+    info = __graft_entry__.build_info("product")
+    if info and info.get("lib_sha256") == __graft_entry__.sha256_file(os.path.realpath(_lib.LIB_PATH)):
+        assert embedded == info["source_sha256"]
+    assert embedded == "" or re.fullmatch(r"[0-9a-f]{64}", embedded), embedded
+
+
 def test_kernels_are_gfx950_code_objects(cfk):
     from cfk_amd import _lib
     blob = open(_lib.LIB_PATH, "rb").read()

@@ -232,6 +232,7 @@ def main(tag, name, launches=None):
         per_side[side] = d
     json.dump({"k": k, "nnz": cfg.get("nnz", 100_000_000), "per_side": per_side, "source": f"profiles/{name}",
                "lib_sha256": bench.get("build", {}).get("lib_sha256"),
+               "device_code_sha256": bench.get("build", {}).get("device_code_sha256"),
                "note": "per launch; hbm_bytes = FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB -> B (Infinity-Cache "
                        "hits are counted by these counters); *_frac over 1024 SIMDs x the launch's GPU cycles "
                        "(GRBM_GUI_ACTIVE / 8 XCDs)"},
