@@ -95,3 +95,51 @@ def test_bench_refuses_the_debug_library(tmp_path, copy):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "refused" in r.stderr, r.stderr[-2000:]
+
+
+def test_prof_summary_sums_the_chunk_launches_of_each_half(tmp_path, monkeypatch):
+    """tools/prof_summary.py on a chunked run (bench config launches_per_half = 2 movie + 3 user launches per
+    iteration): the trace summary and the per-half counters are sums over each half-iteration's launches, in dispatch
+    order, and the counters file is stamped with the profiled library's hashes"""
+    import csv
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import prof_summary
+    monkeypatch.setattr(prof_summary, "ROOT", str(tmp_path))
+    src = tmp_path / "gpurun_out" / "prof_t"
+    main_k = "void cfk::(anonymous namespace)::als_solve_mfma<64, 2, true, false, false, false, 0, false, false>(x)"
+    red_k = "void cfk::(anonymous namespace)::als_solve_mfma<64, 2, false, false, true, false, 0, false, false>(x)"
+    rows, pmc, did, t = [], [], 0, 0
+    for it in range(3):
+        for half, n in (("movie", 2), ("user", 3)):
+            for c in range(n):
+                did += 1
+                dur = 1_000_000 if half == "movie" else 2_000_000   # ns: movie half 2 ms, user half 6 ms
+                rows.append({"Kernel_Name": main_k, "Dispatch_Id": did, "Grid_Size_X": 100 + c,
+                             "Start_Timestamp": t, "End_Timestamp": t + dur})
+                for cnt, v in (("FETCH_SIZE", 10.0), ("WRITE_SIZE", 1.0)):
+                    pmc.append({"Kernel_Name": main_k, "Dispatch_Id": did, "Grid_Size": 100 + c,
+                                "Counter_Name": cnt, "Counter_Value": v})
+                t += dur
+                did += 1
+                rows.append({"Kernel_Name": red_k, "Dispatch_Id": did, "Grid_Size_X": 7,
+                             "Start_Timestamp": t, "End_Timestamp": t + 1000})
+    for sub, data, fields in (("trace/run_kernel_trace.csv", rows, rows[0].keys()),
+                              ("fetch/run_counter_collection.csv", [r for r in pmc if r["Counter_Name"] == "FETCH_SIZE"], pmc[0].keys()),
+                              ("write/run_counter_collection.csv", [r for r in pmc if r["Counter_Name"] == "WRITE_SIZE"], pmc[0].keys())):
+        p = src / sub
+        p.parent.mkdir(parents=True, exist_ok=True)
+        with open(p, "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=list(fields))
+            w.writeheader()
+            w.writerows(data)
+    line = {"config": {"k": 64, "nnz": 1000, "workload_name": "netflix", "launches_per_half": {"movie": 2, "user": 3}},
+            "build": {"lib_sha256": "a" * 64, "device_code_sha256": "d" * 64}}
+    (src / "bench.json").write_text(json.dumps(line) + "\n")
+    prof_summary.main("t", "rT")
+    tr = json.load(open(tmp_path / "profiles" / "rT" / "main_launch_summary.json"))["launches"]
+    assert tr["movie"]["calls"] == 3 and abs(tr["movie"]["avg_ms"] - 2.0) < 1e-9
+    assert tr["user"]["calls"] == 3 and abs(tr["user"]["avg_ms"] - 6.0) < 1e-9
+    c = json.load(open(tmp_path / "profiles" / "counters_k64.json"))
+    assert c["per_side"]["movie"]["hbm_bytes"] == 2 * (10 * 1024 * 2 + 1024)
+    assert c["per_side"]["user"]["hbm_bytes"] == 3 * (10 * 1024 * 2 + 1024)
+    assert c["lib_sha256"] == "a" * 64 and c["device_code_sha256"] == "d" * 64
