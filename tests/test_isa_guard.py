@@ -176,3 +176,27 @@ def test_double_buffered_dma_counts_match_the_vmcnt(kernels):
             assert len(vmem) == 18 and sum(op == "global_load_lds_dwordx4" for op in vmem) == 16, (name, a, len(vmem))
     if not found:
         pytest.skip("no double-buffered pre-split kernel in this build (CFK_PS128_DBUF=0)")
+
+
+def test_fused_dpp_sweep_groups_carry_their_wait_states(kernels):
+    """The sweep's fused row-broadcast FMAs (v_fmac_f32_dpp, inline asm in fmac_rowbcast4): a DPP read of a VGPR
+    needs 2 wait states after a VALU write of it, and the compiler's hazard recognizer does not see the writes inside
+    inline asm, so every group of v_fmac_f32_dpp is preceded and followed by `s_nop 1` (or longer) in the code object."""
+    groups, bad = 0, []
+    for name, ins in _solve_kernels(kernels).items():
+        i = 0
+        while i < len(ins):
+            if ins[i][0] != "v_fmac_f32_dpp":
+                i += 1
+                continue
+            j = i
+            while j < len(ins) and ins[j][0] == "v_fmac_f32_dpp":
+                j += 1
+            groups += 1
+            before, after = ins[i - 1] if i else ("", []), ins[j] if j < len(ins) else ("", [])
+            for op, ops in (before, after):
+                if not (op == "s_nop" and ops and int(ops[0], 0) >= 1):
+                    bad.append((name, i, op, ops))
+            i = j
+    assert groups >= 64, groups
+    assert not bad, bad[:8]
