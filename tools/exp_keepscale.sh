@@ -1,5 +1,5 @@
-# pre-split FULL tasks solved in the table's scaled units (build_ks, CFK_PS_KEEP_SCALE=1) vs the product: the whole
-# -m gpu suite on build_ks, then interleaved kbench at k = 64 / 128
+# pre-split FULL tasks solved in the table scaled units (build_ks, CFK_PS_KEEP_SCALE=1; the variant is not in the tree
+# any more) vs the product: the whole -m gpu suite on build_ks, then interleaved kbench at k = 64 / 128
 set -e
 B=collaborative-filtering-kafka_amd
 CFK_ALS_LIB=$B/build_ks/libcfk_als.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/e23_tests.log 2>&1 || { tail -30 gpurun_out/e23_tests.log; exit 1; }
