@@ -487,6 +487,31 @@ __device__ __forceinline__ void fold_diag(MfmaAcc<C>& acc, f32x4 (&E)[C], int la
     MFMA_DRAIN();
 }
 
+// The same fold with E^T read back transposed from the wave's free LDS image (the pre-split Gram's, 1 KB per tile)
+// instead of 4 C v_mfma_f32_16x16x4_f32 against the identity: (acc + E) + E^T in the same order, bitwise the MFMA
+// fold (each of its outputs is one exact product plus zeros). CFK_FOLD_LDS: the pre-split path (k = 64 / 128 user
+// half -1.6 / -1.8 % in three interleaved rounds, profiles/r05e/e26_*.log).
+#ifndef CFK_FOLD_LDS
+#define CFK_FOLD_LDS 1
+#endif
+template <int C>
+__device__ __forceinline__ void fold_diag_lds(MfmaAcc<C>& acc, const f32x4 (&E)[C], int lane, unsigned char* img) {
+    const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+    for (int b = 0; b < C; ++b) *(f32x4*)(img + b * 1024 + lane * 16) = E[b];   // lane (g, c): E[4g + r][c]
+    wave_sync();
+    // E^T[4g + r][c] = E[c][4g + r]: lane 16 (c >> 2) + 4g + r, component c & 3
+    const int rd = (16 * (c >> 2) + 4 * g) * 16 + (c & 3) * 4;
+#pragma unroll
+    for (int b = 0; b < C; ++b) {
+        f32x4 t = acc.g[tile_index<C>(b, b)];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t[r] = (t[r] + E[b][r]) + *(const float*)(img + b * 1024 + rd + r * 16);
+        acc.g[tile_index<C>(b, b)] = t;
+    }
+    wave_sync();
+}
+
 // ---------------------------------------------------------------------------------------------------
 // Cross-lane moves on the 4 x 16 lane grid (row g = lane >> 4, column c = lane & 15), VALU-only (no LDS)
 // ---------------------------------------------------------------------------------------------------
@@ -1878,7 +1903,12 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
         }
 
         if constexpr (SPLIT && CFK_DIAG_SYM && !NOE) {
-            if constexpr (!REDUCE) fold_diag<C>(acc, E, lane);
+            if constexpr (!REDUCE) {
+                if constexpr (PRESPLIT && CFK_FOLD_LDS)
+                    fold_diag_lds<C>(acc, E, lane, stage_lds[uni(wave)]);   // the image is free after the Gram
+                else
+                    fold_diag<C>(acc, E, lane);
+            }
         }
 
         if (!REDUCE && tk.kind == TASK_PARTIAL) {
