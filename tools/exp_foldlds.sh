@@ -1,5 +1,5 @@
 # diagonal fold through the free LDS image (build_fl, CFK_FOLD_LDS=1) instead of 4 C identity MFMAs vs the product:
-# the whole -m gpu suite on build_fl, then interleaved kbench at k = 64 / 128 (the variant is not in the tree any more)
+# the whole -m gpu suite on build_fl, then interleaved kbench at k = 64 / 128 (CFK_FOLD_LDS=1 is now the default build)
 set -e
 B=collaborative-filtering-kafka_amd
 CFK_ALS_LIB=$B/build_fl/libcfk_als.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/e26_tests.log 2>&1 || { tail -30 gpurun_out/e26_tests.log; exit 1; }
