@@ -91,6 +91,7 @@ SIGNATURES = [
     ("als_debug_copy_partials", _i, [_vp, _vp, _i64, _pi64]),
     ("als_block_path", _i, [_vp, _i, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), _pi64, _pi64]),
     ("als_block_stats", _i, [_vp, _i, _pi64, _pi64, _pi64]),
+    ("als_block_split_info", _i, [_vp, _i, _pi64]),
     # als_host.h
     ("als_dataset_load_netflix", _i, [ctypes.c_char_p, _ppv]),
     ("als_dataset_from_ratings", _i, [_i64, _pi32, _pi32, _pi16, _ppv]),

@@ -64,7 +64,8 @@ struct Block {
     Task* d_sq_tasks = nullptr;     // every FULL + PARTIAL task incl. the short rows (als_sq_error)
     int32_t n_sq = 0;
     bool presplit = false;          // gather a pre-split (scaled fp16 h/m) copy of the opposite table
-    bool rat_exact16 = false;       // every rating of the block is an integer |r| <= 2048 (exact in fp16)
+    // interleaved split rows: rows longer than ilv_chunk entries, blocks permuted chunk-major
+    int64_t ilv_rows = 0, ilv_tasks = 0, ilv_chunk = 0;
     // chunk-major slot layout (als_set_row_layout): local row i -> factor row row_offset + (i / rows_per_chunk) *
     // chunk_stride + i % rows_per_chunk; rows_per_chunk = 0: row_offset + i
     int64_t rows_per_chunk = 0, chunk_stride = 0;
@@ -109,12 +110,10 @@ struct als_engine {
     void* h_stage = nullptr;        // pinned staging of als_write_factors / als_read_factors (copy kernels)
     size_t stage_bytes = 0;
     uint32_t* d_integrity = nullptr;   // cfk::INTEGRITY_WORDS: partial slots that failed their check
-    int* d_queue = nullptr;         // task counter of the pipelined pre-split launch (cfk::launch_solve_pc)
-    unsigned long long* d_pc_stats = nullptr;   // debug build: cycle accounting of the pipelined launch
-    int cu_count = 0;               // compute units of the device: the pipelined launch's grid
-    // pre-split halves through the pipelined launch (Gram waves hand systems to solver waves, cfk::launch_solve_pc)
-    // with ALS_PC=1; default: the one-kernel launch (each wave Gram then solve)
-    bool pipelined = false;
+    int cu_count = 0;               // compute units of the device: the range guard's fallback grid
+    // ALS_INTERLEAVE: interleaved split rows + pre-split Gram for halves whose opposite table outgrows the L2s
+    // (-1 auto, 0 off, 1 wherever the pre-split Gram exists)
+    int interleave = -1;
     uint32_t gen = 0;               // launch generation of the next PARTIAL/REDUCE pair
     int32_t debug_flags = 0;        // debug build only (CFK_DEBUG_KNOBS): ALS_DEBUG_SKIP_SOLVE / _REFINE
     uint32_t debug_gen_skew = 0;    // debug build only: ALS_DEBUG_REDUCE_GEN_SKEW=n, REDUCE decodes with generation
@@ -170,11 +169,6 @@ int sync_checked(als_engine* e) {
     HIP_TRY(hipStreamSynchronize(e->stream));
     uint32_t rec[cfk::INTEGRITY_WORDS];
     HIP_TRY(hipMemcpy(rec, e->d_integrity, sizeof(rec), hipMemcpyDeviceToHost));
-    if (rec[0] != 0 && (int32_t)rec[2] == cfk::PC_TIMEOUT_SLOT)
-        return fail(ALS_ERR_INTEGRITY,
-                    "%u waves of a pipelined launch (generation %u) gave up waiting for a hand-off slot (first: row "
-                    "%d): its results are incomplete",
-                    rec[0], rec[1], (int32_t)rec[3]);
     if (rec[0] != 0)
         return fail(ALS_ERR_INTEGRITY,
                     "%u REDUCE tasks found partial slots that failed their check (first: launch generation %u, slot "
@@ -294,9 +288,6 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
     if (const char* env = getenv("ALS_DEBUG_REDUCE_GEN_SKEW")) e->debug_gen_skew = (uint32_t)atoi(env);
     if (const char* env = getenv("ALS_DEBUG_FIXED_GEN")) e->debug_fixed_gen = env[0] == '1';
     if (const char* env = getenv("ALS_DEBUG_EXTRA_LDS")) e->debug_extra_lds = atoi(env);
-    if (hipMalloc((void**)&e->d_pc_stats, cfk::PC_STAT_N * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(e->d_pc_stats, 0, cfk::PC_STAT_N * sizeof(unsigned long long)) != hipSuccess)
-        e->d_pc_stats = nullptr;
 #endif
     if (const char* env = getenv("ALS_REFINE_MIN_PIVOT")) {
         // the product library can only refine MORE often than the validated gate (> 1: every row); thresholds
@@ -307,7 +298,7 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
 #endif
     }
     if (const char* env = getenv("ALS_DUAL_SIDE")) e->dual_side = env[0] != '0';
-    if (const char* env = getenv("ALS_PC")) e->pipelined = env[0] == '1';
+    if (const char* env = getenv("ALS_INTERLEAVE")) e->interleave = env[0] == '0' ? 0 : 1;
     hipError_t st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (st != hipSuccess) {
         delete e;
@@ -315,14 +306,12 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
     }
     e->own_stream = true;
     st = hipDeviceGetAttribute(&e->cu_count, hipDeviceAttributeMultiprocessorCount, device);
-    if (st == hipSuccess) st = hipMalloc((void**)&e->d_queue, cfk::PC_QUEUE_INTS * sizeof(int));
     if (st == hipSuccess) st = hipMalloc((void**)&e->d_integrity, cfk::INTEGRITY_WORDS * sizeof(uint32_t));
     if (st == hipSuccess) st = hipMemset(e->d_integrity, 0, cfk::INTEGRITY_WORDS * sizeof(uint32_t));
     if (st == hipSuccess) st = hipMalloc((void**)&e->d_amax, 2 * sizeof(uint32_t));
     if (st != hipSuccess) {
         (void)hipStreamDestroy(e->stream);
         (void)hipFree(e->d_integrity);
-        (void)hipFree(e->d_queue);
         (void)hipFree(e->d_amax);
         delete e;
         return fail(ALS_ERR_DEVICE, "integrity record: %s", hipGetErrorString(st));
@@ -342,8 +331,6 @@ int als_engine_destroy(als_engine* e) {
     (void)hipFree(e->d_split);
     (void)hipHostFree(e->h_stage);
     (void)hipFree(e->d_integrity);
-    (void)hipFree(e->d_queue);
-    (void)hipFree(e->d_pc_stats);
     (void)hipFree(e->d_amax);
     for (auto& rec : e->pending)
         for (auto ev : rec.ev) (void)hipEventDestroy(ev);
@@ -421,20 +408,34 @@ int check_block_shape(als_engine* e, int64_t n_rows, int64_t row_offset, int64_t
 }
 
 // Padded entries of a row of degree d (every row starts on a 32-entry block).
-// every rating r satisfies |r| <= 2048, so rh = fp16(r) = r and rm = 0 (the pre-split RHS can skip the rm pairs)
-bool ratings_exact16(const int16_t* r, int64_t n) {
-    for (int64_t i = 0; i < n; ++i)
-        if (r[i] > 2048 || r[i] < -2048) return false;
-    return true;
-}
 inline int64_t padded(int64_t d) { return (d + cfk::BLOCK_ENTRIES - 1) / cfk::BLOCK_ENTRIES * cfk::BLOCK_ENTRIES; }
+
+// Interleaved split rows: on a half whose opposite table outgrows the L2s (> 32 MB: the 123 MB
+// user table of the Netflix-shape movie half), a row longer than the returned length (entries) is split into
+// nc = ceil(d / length) chunks of INTERLEAVED blocks -- chunk c = blocks c, c + nc, c + 2 nc, ... of the row -- so
+// that every chunk covers the row's whole range of opposite slots. With the chunks dispatched together (longest
+// first) the waves of an XCD then walk the opposite table in step and find its rows in their L2. Such a half gathers
+// the pre-split table (the fp16 Gram). 0: contiguous chunks at chunk_entries() (the other halves).
+int64_t interleave_chunk(const als_engine* e, int64_t n_opp_rows) {
+    const int64_t sb = (n_opp_rows + 1) * (int64_t)cfk::presplit_row_bytes(e->kp);
+    if (e->interleave == 0 || e->path != Path::MFMA_SPLIT || (e->kp != 64 && e->kp != 128)) return 0;
+    if (n_opp_rows + 1 >= (1 << 24) || sb > (int64_t)UINT32_MAX) return 0;   // the pre-split gather's offsets
+    if (e->interleave < 0 && sb <= (32ll << 20)) return 0;
+    // chunk length (kbench, Netflix shape, movie half + its REDUCE, profiles/r06a): k = 64 8,192 / 10,240 / 12,288 /
+    // 16,384 / 24,576 entries: 2.07 / 2.04 / 2.06 / 2.16 / 2.29 ms (contiguous chunks: 2.98); k = 128 4,096 / 8,192 /
+    // 16,384: 5.76 / 5.32 / 5.06 ms (contiguous: 6.67)
+    int64_t len = e->kp == 128 ? 16384 : 10240;
+#ifdef CFK_DEBUG_KNOBS
+    if (const char* v = getenv("ALS_ILV_CHUNK")) len = std::max(32L, atol(v));
+#endif
+    return (len + cfk::BLOCK_ENTRIES - 1) / cfk::BLOCK_ENTRIES * cfk::BLOCK_ENTRIES;
+}
 
 // Work plan of a block whose padded in-block (d_col / d_rat, device, already laid out) has row degrees deg[]
 // and row starts begin[]: FULL / PARTIAL / REDUCE tasks, longest first; uploads the plan, takes ownership of
 // d_col / d_rat and sizes the partial and pre-split workspaces.
 int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows, int64_t nnz,
-                 const std::vector<int64_t>& deg, const std::vector<int64_t>& begin, int32_t* d_col, float* d_rat,
-                 bool rat_exact16) {
+                 const std::vector<int64_t>& deg, const std::vector<int64_t>& begin, int32_t* d_col, float* d_rat) {
     const int64_t nnz_padded = begin[n_rows];
     auto drop = [&]() {
         (void)hipFree(d_col);
@@ -442,9 +443,55 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     };
     // the generic path's workgroup takes a whole row of any length: no split rows
     const int64_t chunk = e->path == Path::GENERIC ? INT64_MAX : chunk_entries(nnz_padded);
-    std::vector<Task> tasks, reduce;
+    std::vector<Task> tasks, reduce, stasks;
     int64_t slots = 0;
+    // Interleaved split rows: the long rows' blocks are permuted chunk-major (chunk c = blocks c, c + nc, ... of the
+    // row, in order), each chunk one PARTIAL task of whole blocks (the row's last, padded block is the last block of
+    // its chunk, so nent counts exactly the chunk's real entries), one REDUCE per row.
+    const int64_t ilv = interleave_chunk(e, n_opp_rows);
+    std::vector<int32_t> perm;
+    int64_t ilv_rows = 0;
+    if (ilv > 0) {
+        constexpr int64_t BE = cfk::BLOCK_ENTRIES;
+        for (int64_t i = 0; i < n_rows; ++i) {
+            const int64_t d = deg[i];
+            if (d <= ilv) continue;
+            if (perm.empty()) {
+                perm.resize((size_t)(nnz_padded / BE));
+                for (size_t q = 0; q < perm.size(); ++q) perm[q] = (int32_t)q;
+            }
+            ++ilv_rows;
+            const int64_t nb = (d + BE - 1) / BE, nc = (d + ilv - 1) / ilv, b0 = begin[i] / BE;
+            Task t{};
+            t.row = (int32_t)i;
+            t.ndeg = (int32_t)d;
+            t.kind = cfk::TASK_PARTIAL;
+            const int64_t first = slots;
+            int64_t pos = 0;
+            for (int64_t c = 0; c < nc; ++c) {
+                const int64_t p0 = pos;
+                for (int64_t x = c; x < nb; x += nc) perm[(size_t)(b0 + pos++)] = (int32_t)(b0 + x);
+                const int64_t cnt = pos - p0;
+                const bool last = (nb - 1) % nc == c;
+                const int64_t nent = last ? BE * (cnt - 1) + (d - BE * (nb - 1)) : BE * cnt;
+                Task p = t;
+                p.begin = begin[i] + BE * p0;
+                p.nent = (int32_t)nent;
+                p.nsteps = (int32_t)((nent + 3) / 4);
+                p.slot = (int32_t)slots++;
+                stasks.push_back(p);
+            }
+            Task r = t;
+            r.begin = 0;
+            r.slot = (int32_t)first;
+            r.nsteps = (int32_t)(slots - first);
+            r.kind = cfk::TASK_REDUCE;
+            reduce.push_back(r);
+        }
+    }
+    const int64_t ilv_tasks = (int64_t)stasks.size();
     for (int64_t i = 0; i < n_rows; ++i) {
+        if (ilv > 0 && deg[i] > ilv) continue;   // interleaved above
         const int64_t d = deg[i];
         Task t{};
         t.row = (int32_t)i;
@@ -480,7 +527,8 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     // Y Y^T + lambda n I_n has the nonzero spectrum of Y^T Y + lambda n I_k plus nothing smaller, so the same
     // conditioning; with n > k the n x n system would carry n - k eigenvalues lambda n only (singular at
     // lambda = 0 where the reference's k x k system is not). ALS_DUAL=0 turns it off.
-    std::vector<Task> sq_all = tasks;
+    std::vector<Task> sq_all = stasks;
+    sq_all.insert(sq_all.end(), tasks.begin(), tasks.end());
     std::vector<Task> dual[3];
     {
         const int max_cd = e->path != Path::MFMA_SPLIT ? 0 : e->kp == 128 ? 6 : e->kp == 64 ? 2 : 0;
@@ -504,8 +552,9 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     }
     // Longest tasks first (LPT): the grid drains with a short tail.
     std::stable_sort(tasks.begin(), tasks.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
-    // ALS_TASK_ORDER=random / stagger[:W] (measurement knobs): a seeded shuffle of the main launch's tasks, or LPT
-    // windows alternating between its longer and shorter half
+#ifdef CFK_DEBUG_KNOBS
+    // ALS_TASK_ORDER=random / stagger[:W] (measurement knobs, debug build only): a seeded shuffle of the main launch's
+    // tasks, or LPT windows alternating between its longer and shorter half
     if (const char* env = getenv("ALS_TASK_ORDER")) {
         if (std::strncmp(env, "stagger", 7) == 0) {
             // windows of W tasks (W = stagger:<W>, default 1024 = one 4-wave workgroup per CU) alternate between the
@@ -531,12 +580,38 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
             }
         }
     }
+#endif
     std::stable_sort(reduce.begin(), reduce.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
     for (auto& d : dual)
         std::stable_sort(d.begin(), d.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
 
+    // the interleaved chunks join the plain tasks, longest first
+    if (!stasks.empty()) {
+        tasks.insert(tasks.begin(), stasks.begin(), stasks.end());
+        std::stable_sort(tasks.begin(), tasks.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
+    }
+
     hipError_t st0 = hipSetDevice(e->device);
     if (st0 == hipSuccess) st0 = hipStreamSynchronize(e->stream);
+    if (st0 == hipSuccess && !perm.empty()) {
+        // the long rows' blocks chunk-major (before the pre-split packing below derives its arrays from them)
+        int32_t *d_perm = nullptr, *col2 = nullptr;
+        float* rat2 = nullptr;
+        st0 = hipMalloc((void**)&d_perm, perm.size() * 4);
+        if (st0 == hipSuccess) st0 = hipMalloc((void**)&col2, (size_t)nnz_padded * 4);
+        if (st0 == hipSuccess) st0 = hipMalloc((void**)&rat2, (size_t)nnz_padded * 4);
+        if (st0 == hipSuccess) st0 = hipMemcpy(d_perm, perm.data(), perm.size() * 4, hipMemcpyHostToDevice);
+        if (st0 == hipSuccess)
+            st0 = cfk::launch_permute_blocks(d_col, d_rat, col2, rat2, d_perm, (int64_t)perm.size(), nullptr);
+        if (st0 == hipSuccess) st0 = hipDeviceSynchronize();
+        (void)hipFree(d_perm);
+        if (st0 == hipSuccess) {
+            std::swap(d_col, col2);
+            std::swap(d_rat, rat2);
+        }
+        (void)hipFree(col2);
+        (void)hipFree(rat2);
+    }
     if (st0 != hipSuccess) {
         drop();
         return fail(ALS_ERR_DEVICE, "set_block: %s", hipGetErrorString(st0));
@@ -563,13 +638,12 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     {
         const int64_t sb = (n_opp_rows + 1) * (int64_t)cfk::presplit_row_bytes(e->kp);
         const bool ps_kp = e->path == Path::MFMA_SPLIT && (e->kp == 64 || e->kp == 128);
-        bool ps = ps_kp && (e->kp == 128 || sb <= (8ll << 20));
+        bool ps = ps_kp && (e->kp == 128 || sb <= (8ll << 20) || ilv > 0);
         if (const char* env = getenv("ALS_PRESPLIT")) ps = ps_kp && env[0] == '1';
         // the pre-split gather forms 32-bit byte offsets row * presplit_row_bytes with a 24-bit multiply: both the
         // row (< 2^24) and the offset (< 2^32) must fit, also when ALS_PRESPLIT=1 forces the path
         if (n_opp_rows + 1 >= (1 << 24) || sb > (int64_t)UINT32_MAX) ps = false;
         blk.presplit = ps;
-        blk.rat_exact16 = rat_exact16;
         if (ps && (size_t)sb > e->split_bytes) {
             (void)hipFree(e->d_split);
             e->d_split = nullptr;
@@ -602,6 +676,9 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     };
     int r;
     if ((r = up((void**)&blk.d_tasks, tasks.data(), tasks.size() * sizeof(Task)))) return r;
+    blk.ilv_rows = ilv_rows;
+    blk.ilv_tasks = ilv_tasks;
+    blk.ilv_chunk = ilv;
     if ((r = up((void**)&blk.d_reduce, reduce.data(), reduce.size() * sizeof(Task)))) return r;
     for (int c = 0; c < 3; ++c) {
         if ((r = up((void**)&blk.d_dual[c], dual[c].data(), dual[c].size() * sizeof(Task)))) return r;
@@ -689,7 +766,7 @@ int als_set_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, i
             return fail(ALS_ERR_OUT_OF_MEMORY, "in-block upload: %s", hipGetErrorString(st));
         }
     }
-    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat, ratings_exact16(ratings, nnz));
+    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat);
 }
 
 int als_set_block_coo(als_engine* e, int side, int64_t n_rows, int64_t row_offset, int64_t n_opp_rows, int64_t nnz,
@@ -708,7 +785,7 @@ int als_set_block_coo(als_engine* e, int side, int64_t n_rows, int64_t row_offse
     const int code = cfk::build_block_device(rows, cols, ratings, nnz, n_rows, n_opp_rows, e->stream, deg, begin,
                                              &d_col, &d_rat, err);
     if (code != ALS_OK) return fail(code, "als_set_block_coo: %s", err.c_str());
-    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat, ratings_exact16(ratings, nnz));
+    return finish_block(e, side, n_rows, row_offset, n_opp_rows, nnz, deg, begin, d_col, d_rat);
 }
 
 int als_alloc_factors(als_engine* e, int side, int64_t n_total_rows) {
@@ -902,14 +979,8 @@ int launch_half(als_engine* e, int side, float lambda, const Task* tasks, int32_
         a.rat_lo_off = b.nnz_padded / 2;
         a.col_ps = b.d_col_ps;
         a.amax = e->d_amax;
-        a.rat_exact16 = b.rat_exact16 ? 1 : 0;
     }
-    a.queue = e->d_queue;
-    a.pc_stats = e->d_pc_stats;
-    if (b.presplit && e->pipelined)
-        HIP_TRY(cfk::launch_solve_pc(e->kp, a, e->cu_count, e->stream));
-    else
-        HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.presplit, false));
+    HIP_TRY(cfk::launch_solve(e->precision, e->kp, e->path, a, e->stream, b.presplit, false));
     if (b.presplit) {
         // the range guard's fallback: the same tasks on the fp32 table with the on-the-fly split, a launch whose
         // waves exit at once unless the opposite table is out of the pre-split's range (cfk::presplit_ok)
@@ -1339,21 +1410,22 @@ int als_block_stats(const als_engine* e, int side, int64_t* n_tasks, int64_t* n_
     return ALS_OK;
 }
 
+int als_block_split_info(const als_engine* e, int side, int64_t info[4]) {
+    if (int r = check_engine(e)) return r;
+    if (int r = check_side(side)) return r;
+    if (!info) return fail(ALS_ERR_INVALID_ARGUMENT, "info is NULL");
+    const Block& b = e->blk[side];
+    info[0] = b.ilv_rows;
+    info[1] = b.ilv_tasks;
+    info[2] = b.ilv_chunk;
+    info[3] = b.presplit ? 1 : 0;
+    return ALS_OK;
+}
+
 }  // extern "C"
 
 #ifdef CFK_DEBUG_KNOBS
 // Debug build only (not in include/als.h): present iff the work-dropping / fault-injection knobs are compiled in
 // (bench.py refuses a library that exports it, whatever its path).
 extern "C" int als_debug_knobs_compiled(void) { return 1; }
-// Debug build only (not in include/als.h): read (and with reset, zero) the pipelined launch's cycle accounting,
-// cfk::PC_STAT_N counters (tools/kbench.py --pc-stats).
-extern "C" int als_debug_pc_stats(als_engine* e, unsigned long long* out, int reset) {
-    if (int r = check_engine(e)) return r;
-    if (!e->d_pc_stats) return fail(ALS_ERR_STATE, "no pipelined-launch statistics");
-    HIP_TRY(hipSetDevice(e->device));
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    HIP_TRY(hipMemcpy(out, e->d_pc_stats, cfk::PC_STAT_N * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    if (reset) HIP_TRY(hipMemset(e->d_pc_stats, 0, cfk::PC_STAT_N * sizeof(unsigned long long)));
-    return ALS_OK;
-}
 #endif

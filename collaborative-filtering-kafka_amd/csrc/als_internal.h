@@ -71,9 +71,6 @@ struct SolveArgs {
     int32_t presplit_fallback;  // the on-the-fly split launch guarding a pre-split half: it runs only when the table
                                 //   is out of the pre-split's range (presplit_ok(amax) false), else exits at once
     int64_t scratch_slabs;  // generic path: workgroup slabs in `partials` (its Gram when it does not fit in LDS)
-    int* queue;             // pipelined launch (als_solve_pc): PC_QUEUE_INTS task counters (zeroed by launch_solve_pc)
-    unsigned long long* pc_stats;   // debug build only (else null): PC_STAT_* cycle counters of the pipelined launch
-    int32_t rat_exact16;    // presplit: every rating is exact in fp16 (|r| <= 2048): r = rh, rm = 0
     int32_t grid_cap;       // workgroups of a grid-stride launch (the range guard's fallback): CUs x 4
     int32_t extra_lds;      // diagnostics (debug build's ALS_DEBUG_EXTRA_LDS, else 0): unused dynamic LDS per workgroup
 };
@@ -87,17 +84,6 @@ __host__ __device__ inline int64_t factor_row(int64_t row_offset, int32_t rows_p
 // Partial-slot integrity record (device, 4 words): [0] REDUCE tasks that found a bad slot, [1] generation, [2] slot,
 // [3] row of the first failure. Read back by every synchronising call of the engine.
 constexpr int INTEGRITY_WORDS = 4;
-// Slot value of an integrity record written by the pipelined launch (als_solve_pc) when a wave's hand-off wait ran
-// out of time (a protocol failure, not a partial slot).
-constexpr int32_t PC_TIMEOUT_SLOT = -2;
-// Task queue of the pipelined launch: PC_STREAMS counters (stream x = tasks x, x + PC_STREAMS, ...), one 128-B line
-// each, PC_CHUNK stream positions per atomic; SolveArgs::queue holds PC_QUEUE_INTS ints.
-constexpr int PC_STREAMS = 8, PC_QSTRIDE = 32, PC_CHUNK = 8;
-constexpr int PC_QUEUE_INTS = PC_STREAMS * PC_QSTRIDE;
-// Debug-build cycle accounting of the pipelined launch (s_memtime, summed over waves): Gram waves' Gram cycles and
-// cycles waiting for a free slot, solver waves' solve cycles and idle (polling) cycles, systems solved, tasks.
-enum { PC_STAT_GRAM = 0, PC_STAT_GRAM_WAIT, PC_STAT_SOLVE, PC_STAT_SOLVE_IDLE, PC_STAT_SOLVES, PC_STAT_TASKS,
-       PC_STAT_T_SETUP, PC_STAT_T_SCALE, PC_STAT_T_FACTOR, PC_STAT_T_SUBST, PC_STAT_T_END, PC_STAT_N = 16 };
 // Diagnostic: skip the k x k solve after the Gram (stores the Gram diagonal instead) -- used by
 // tools/kbench.py to split a launch's time into Gram and solve. Only the debug build (CFK_DEBUG_KNOBS) can set
 // these flags; the product library never does.
@@ -141,9 +127,9 @@ hipError_t launch_generic(int precision, int kp, const SolveArgs& a, hipStream_t
 // same half).
 hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hipStream_t s, bool presplit,
                         bool reduce);
-// Pipelined pre-split launch (als_solve_pc, kp 64 or 128): persistent, one workgroup per CU (cu_count), Gram waves
-// hand FULL systems to solver waves through LDS; same tasks and results as launch_solve(..., presplit = true, false).
-hipError_t launch_solve_pc(int kp, const SolveArgs& a, int cu_count, hipStream_t s);
+// Block permutation of the in-block (32-entry blocks): dst block i <- src block perm[i] (cols and ratings).
+hipError_t launch_permute_blocks(const int32_t* col, const float* rat, int32_t* col_out, float* rat_out,
+                                 const int32_t* perm, int64_t n_blocks, hipStream_t s);
 // Short rows in entry space (als_solve_dual): fp32 split path, kp 64 with cd 2, kp 128 with cd 2 or 4 (rows of
 // 16 * cd padded entries, i.e. cd / 2 blocks); `a.tasks` are FULL tasks of such rows.
 hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s);

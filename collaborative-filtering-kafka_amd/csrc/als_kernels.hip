@@ -386,10 +386,6 @@ __device__ __forceinline__ f32x4 mfma_f16(const u32x4& a, const u32x4& b, f32x4 
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
                                                   0);
 }
-// c + a.lo b.lo + a.hi b.hi on fp16 pairs (v_dot2_f32_f16; the fp16 x fp16 products are exact in fp32)
-__device__ __forceinline__ float dot2_f16(unsigned a, unsigned b, float c) {
-    return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, a), __builtin_bit_cast(f16x2, b), c, false);
-}
 // Scale exponent s of a pre-split table from the bits of its largest |x| (als_absmax): 2^s max|x| <= 2^14 < the fp16
 // maximum 65504 (no overflow at any rounding), and the table's values use the whole fp16 range (m stays normal for
 // |x| >= 2^-17 max|x|). A zero, infinite or NaN maximum keeps s = 0; s is clamped so 2^s and 2^-2s stay usable.
@@ -415,25 +411,12 @@ __device__ __forceinline__ int split_exp(uint32_t maxbits) {
         static_for<0, CFK_DRAIN_NOPS>([&](auto) { asm volatile("s_nop 7"); }); \
         __builtin_amdgcn_sched_barrier(0);                                    \
     } while (0)
-// RHS of the on-the-fly split path: computed before its block's MFMA group and materialised there (1), or
-// after it (0). With 0 (and SLP-vectorised packed-fp32 VALU), LLVM deferred the RHS products into v_pk_mul /
+// RHS of the on-the-fly split path: computed before its block's MFMA group and materialised there. Computed
+// after it (and with SLP-vectorised packed-fp32 VALU), LLVM deferred the RHS products into v_pk_mul /
 // v_pk_add_f32 chains next to the next block's MFMAs, and on gfx950 that intermittently lost ~1/3 of RHS
 // component 3 in lanes 48..63 of a wave (tools/split_diag.py: 5 of 5 captured failures had this signature;
 // 9 wrong movie rows in 300 Netflix-shape halves). Both this and building the kernels without SLP
 // vectorisation (Makefile) remove it (0 in 300 halves each).
-#ifndef CFK_RHS_EARLY
-#define CFK_RHS_EARLY 1
-#endif
-// KP = 128 split Gram: split VALU interleaved into the MFMA issue gaps (column-order tiles), or (0) the plain
-// split_step of the other widths.
-#ifndef CFK_K128_INTERLEAVE
-#define CFK_K128_INTERLEAVE 1
-#endif
-// The solve's v_mfma_f32_16x16x4_f32 groups get the same treatment when CFK_SOLVE_DRAIN is set.
-#ifndef CFK_SOLVE_DRAIN
-#define CFK_SOLVE_DRAIN 0
-#endif
-__device__ __forceinline__ void pin4(f32x4& v) { asm volatile("" : "+v"(v)); }
 
 template <int C>
 struct MfmaAcc {
@@ -449,9 +432,6 @@ __host__ __device__ constexpr int tile_index(int b1, int b2) { return b1 * C - (
 // Diagonal tiles of the split Gram: hm + mh = X + X^T and hl + lh = Y + Y^T with X = h m^T, Y = h l^T, so the
 // split paths accumulate X + Y per diagonal tile in E (2 MFMAs instead of 4 per block) and fold
 // G_bb += E_b + E_b^T once per task: 8 of the 60 Gram MFMAs per block saved.
-#ifndef CFK_DIAG_SYM
-#define CFK_DIAG_SYM 1
-#endif
 
 // G_bb += E_b + E_b^T. E^T via v_mfma_f32_16x16x4_f32 against the identity: with both operands in accumulator
 // layout the four k-slices compute D += E^T I (see solve_tiles), each output one exact product plus C.
@@ -487,26 +467,29 @@ __device__ __forceinline__ void fold_diag(MfmaAcc<C>& acc, f32x4 (&E)[C], int la
     MFMA_DRAIN();
 }
 
-// The same fold with E^T read back transposed from the wave's free LDS image (the pre-split Gram's, 1 KB per tile)
-// instead of 4 C v_mfma_f32_16x16x4_f32 against the identity: (acc + E) + E^T in the same order, bitwise the MFMA
-// fold (each of its outputs is one exact product plus zeros). CFK_FOLD_LDS: the pre-split path (k = 64 / 128 user
-// half -1.6 / -1.8 % in three interleaved rounds, profiles/r05e/e26_*.log).
-#ifndef CFK_FOLD_LDS
-#define CFK_FOLD_LDS 1
-#endif
+// The same fold with E^T read back transposed from the wave's free LDS image (the pre-split Gram's) instead of 4 C
+// v_mfma_f32_16x16x4_f32 against the identity: (acc + E) + E^T in the same order, bitwise the MFMA fold (each of its
+// outputs is one exact product plus zeros). The pre-split path uses it (k = 64 / 128 user half -1.6 / -1.8 % in three
+// interleaved rounds, profiles/r05e/e26_*.log). Bank-conflict-free image (round 6): lane (g, c) stores its column
+// piece E[4g .. 4g+3][c] as one ds_write_b128 at dword 20 c + 4 g of its tile's 1280-B region, so the eight lanes of
+// every b128 write group cover the 32 banks once; lane (g, c) then reads E[c][4g + r] with ds_read_b32 at dword
+// 20 (4g + r) + 4 (c >> 2) + (c & 3) = 80 g + 20 r + c: 32 distinct banks per 32-lane group. (Round 5 read a
+// 16-dword-stride image: 4-way conflicts, SQ_LDS_BANK_CONFLICT 0.118 of the user launch's LDS cycles.)
+constexpr int FOLD_TILE_BYTES = 1280;
 template <int C>
 __device__ __forceinline__ void fold_diag_lds(MfmaAcc<C>& acc, const f32x4 (&E)[C], int lane, unsigned char* img) {
+    static_assert(C * FOLD_TILE_BYTES <= 2 * C * 1024, "fold image within the wave's LDS-DMA image");
     const int g = lane >> 4, c = lane & 15;
 #pragma unroll
-    for (int b = 0; b < C; ++b) *(f32x4*)(img + b * 1024 + lane * 16) = E[b];   // lane (g, c): E[4g + r][c]
+    for (int b = 0; b < C; ++b) *(f32x4*)(img + b * FOLD_TILE_BYTES + (20 * c + 4 * g) * 4) = E[b];
     wave_sync();
-    // E^T[4g + r][c] = E[c][4g + r]: lane 16 (c >> 2) + 4g + r, component c & 3
-    const int rd = (16 * (c >> 2) + 4 * g) * 16 + (c & 3) * 4;
+    const int rd = (80 * g + c) * 4;
 #pragma unroll
     for (int b = 0; b < C; ++b) {
         f32x4 t = acc.g[tile_index<C>(b, b)];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) t[r] = (t[r] + E[b][r]) + *(const float*)(img + b * 1024 + rd + r * 16);
+        for (int r = 0; r < 4; ++r)
+            t[r] = (t[r] + E[b][r]) + *(const float*)(img + b * FOLD_TILE_BYTES + rd + r * 80);
         acc.g[tile_index<C>(b, b)] = t;
     }
     wave_sync();
@@ -528,20 +511,6 @@ __device__ __forceinline__ float col_bcast(float v) {
     const int addr = ((int)(__lane_id() & 15) + 16 * G) * 4;
     return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
 }
-// the same broadcast with two VALU lane swaps (v_permlane16_swap: even/odd row of each pair; v_permlane32_swap:
-// low/high pair), no LDS round trip: shorter latency, but both operands are rewritten (register copies)
-template <int G>
-__device__ __forceinline__ float col_bcast_swap(float v) {
-    const auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
-    const int w = (int)s16[G & 1];
-    const auto s32 = __builtin_amdgcn_permlane32_swap(w, w, false, false);
-    return __int_as_float((int)s32[G >> 1]);
-}
-// CFK_COL_SWAP: sweep column broadcasts by lane swaps for KP >= this (one wave per SIMD at KP = 128, where the
-// pivot chain's latency is exposed), by ds_bpermute below it
-#ifndef CFK_COL_SWAP
-#define CFK_COL_SWAP 1000
-#endif
 
 // sum over the 4 rows at each column, result in every row
 __device__ __forceinline__ float col_sum(float v) {
@@ -568,14 +537,11 @@ __device__ __forceinline__ float row_sum_to_last(float v) {
 // a[i][p] + a[i][p] (d - 1)(-1/d) = a[i][p] / d. That FMA is accurate to a few ulp only while d <= 1,
 // which the caller guarantees by Jacobi-scaling the system to a unit diagonal (every later pivot is a
 // Schur-complement diagonal of a unit-diagonal SPD matrix, so it stays in (0, 1]).
-// CFK_SWEEP_DPPFMA: the four row broadcasts fused into the FMAs (v_fmac_f32_dpp row_newbcast, one instruction per
-// register instead of a v_mov_b32_dpp + v_fmac_f32 pair; k = 64 / 128 user half -3 %, profiles/r05e/e18_*.log).
+// The four row broadcasts are fused into the FMAs (v_fmac_f32_dpp row_newbcast, one instruction per register
+// instead of a v_mov_b32_dpp + v_fmac_f32 pair; k = 64 / 128 user half -3 %, profiles/r05e/e18_*.log).
 // A DPP read of a VGPR needs 2 wait states after a VALU write of it, and the compiler's hazard recognizer does not
 // see VALU writes inside inline asm: the block waits 2 states before its first DPP read (the previous step's writes)
 // and after its last write (a compiler-placed DPP or lane op reading the results next).
-#ifndef CFK_SWEEP_DPPFMA
-#define CFK_SWEEP_DPPFMA 1
-#endif
 template <int L>
 __device__ __forceinline__ void fmac_rowbcast4(f32x4& a, float t) {
     float a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
@@ -592,62 +558,30 @@ __device__ __forceinline__ void fmac_rowbcast4(f32x4& a, float t) {
     a[2] = a2;
     a[3] = a3;
 }
-template <bool SWAP, int p>
+template <int p>
 __device__ __forceinline__ void sweep_step(f32x4& a, int lane, float& nrd_min) {
     constexpr int pg = p >> 2, pr = p & 3;
     const float nrd = __builtin_amdgcn_rcpf(-bcast(a[pr], 16 * pg + p));   // -1 / d
     nrd_min = fminf(nrd_min, nrd);                                          // -1 / (smallest pivot)
     const bool piv = lane == 16 * pg + p;   // 16 lane masks, CSE-d across the 4 diagonal tiles (SGPRs)
     a[pr] = piv ? a[pr] - 1.f : a[pr];
-    const float t = (SWAP ? col_bcast_swap<pg>(a[pr]) : col_bcast<pg>(a[pr])) * nrd;   // a[p][c] (d - 1 at c = p) * (-1/d)
-    if constexpr (CFK_SWEEP_DPPFMA) {
-        fmac_rowbcast4<p>(a, t);   // a[4g + r][c] += a[4g + r][p] t[c]
-    } else {
-        f32x4 cp;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cp[r] = row_lane_bcast<p>(a[r]);   // a[4g + r][p] (d - 1 at row p)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) a[r] += cp[r] * t;
-    }
+    const float t = col_bcast<pg>(a[pr]) * nrd;   // a[p][c] (d - 1 at c = p) * (-1/d)
+    fmac_rowbcast4<p>(a, t);                       // a[4g + r][c] += a[4g + r][p] t[c]
     a[pr] = piv ? nrd : a[pr];
 }
-template <bool SWAP>
 __device__ __forceinline__ void sweep_tile(f32x4& a, int lane, float& nrd_min) {
-    static_for<0, 16>([&](auto P_) { sweep_step<SWAP, decltype(P_)::value>(a, lane, nrd_min); });
+    static_for<0, 16>([&](auto P_) { sweep_step<decltype(P_)::value>(a, lane, nrd_min); });
 }
 
 // D + X^T Y of two 16 x 16 tiles in accumulator layout (the solve's block products): four v_mfma_f32_16x16x4_f32
-// (exact fp32 products, 128 MFMA cycles), or -- CFK_SOLVE_SPLIT -- both operands split exactly into three bf16 terms
-// (split3) and the six partial products hh, mh, hm, mm, hl, lh in three v_mfma_f32_16x16x32_bf16 (48 cycles): lane
-// (g, c)'s eight k slots of the 16x16x32 operand are its four rows 4g + r of column c in two terms, so X^T Y needs no
-// lane movement; each bf16 product is exact in fp32 and the dropped ml, lm, ll terms are below 2^-26 |xy|.
-#ifndef CFK_SOLVE_SPLIT
-#define CFK_SOLVE_SPLIT 0
-#endif
+// (exact fp32 products, 128 MFMA cycles)
 __device__ __forceinline__ f32x4 tile_tn(const f32x4& X, const f32x4& Y, f32x4 D) {
-    if constexpr (CFK_SOLVE_SPLIT) {
-        unsigned xh0, xm0, xl0, xh1, xm1, xl1, yh0, ym0, yl0, yh1, ym1, yl1;
-        split3(X[0], X[1], xh0, xm0, xl0);
-        split3(X[2], X[3], xh1, xm1, xl1);
-        split3(Y[0], Y[1], yh0, ym0, yl0);
-        split3(Y[2], Y[3], yh1, ym1, yl1);
-        const u32x4 ahl = {xh0, xh1, xl0, xl1}, ahm = {xh0, xh1, xm0, xm1};
-        const u32x4 blh = {yl0, yl1, yh0, yh1}, bmm = {ym0, ym1, ym0, ym1}, bhh = {yh0, yh1, yh0, yh1};
-        __builtin_amdgcn_sched_barrier(0);
-        D = mfma_k32(ahl, blh, D);   // hl + lh
-        D = mfma_k32(ahm, bmm, D);   // hm + mm
-        D = mfma_k32(ahm, bhh, D);   // hh + mh
-        MFMA_DRAIN();
-        asm volatile("" ::"v"(ahl), "v"(ahm), "v"(blh), "v"(bmm), "v"(bhh));   // operands live past the drain
-        return D;
-    } else {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) D = __builtin_amdgcn_mfma_f32_16x16x4f32(X[s], Y[s], D, 0, 0, 0);
-        return D;
-    }
+    for (int s = 0; s < 4; ++s) D = __builtin_amdgcn_mfma_f32_16x16x4f32(X[s], Y[s], D, 0, 0, 0);
+    return D;
 }
 
-// Lookahead schedule of the block factorisation (CFK_SOLVE_LOOKAHEAD): step P first finishes block column P + 1
+// Lookahead schedule of the block factorisation: step P first finishes block column P + 1
 // (V'_{P,P+1} and the update of T_{P+1,P+1}), so the 16-step sweep of T_{P+1,P+1} -- a dependent chain of
 // broadcasts, latency-bound -- can start at once, and the rest of step P's MFMA work (block columns J >= P + 2) is
 // issued between its steps. Items of step P, J descending, per J: V'_PJ = S_P T_PJ, then T_IJ += T_PI^T V'_PJ for
@@ -671,33 +605,9 @@ __host__ __device__ constexpr int la_item_I(int C, int P, int t) {   // -1: the 
     }
     return -2;
 }
-// waves per SIMD of the pre-split KP = 64 kernel (register budget 512 / waves; LDS 16 x 8.25 KB at 4)
-#ifndef CFK_PS64_WAVES
-#define CFK_PS64_WAVES 4
-#endif
-// One-kernel pre-split launch at KP = 128: LDS-DMA two blocks ahead into two images (gram_presplit's DBUF)
-#ifndef CFK_PS128_DBUF
-#define CFK_PS128_DBUF 0
-#endif
-// One-kernel pre-split launch: the RHS by v_dot2_f32_f16 instead of 2 C MFMA tiles (gram_presplit's RHS mode)
-#ifndef CFK_PS_DOT2
-#define CFK_PS_DOT2 0
-#endif
-// Pipelined launch: the solver waves' issue priority (s_setprio) and their sweep column broadcasts (1: lane swaps,
-// the shorter latency; 0: ds_bpermute)
-#ifndef CFK_PC_PRIO
-#define CFK_PC_PRIO 1
-#endif
-#ifndef CFK_PC_SWAP
-#define CFK_PC_SWAP 0
-#endif
-// Gram waves of the 16-wave pipelined pre-split KP = 64 workgroup (the rest solve)
-#ifndef CFK_PC64_NG
-#define CFK_PC64_NG 12
-#endif
-#ifndef CFK_SOLVE_LOOKAHEAD
-#define CFK_SOLVE_LOOKAHEAD 1
-#endif
+// waves per SIMD of the pre-split KP = 64 kernel (register budget 512 / waves; LDS 16 x 8.25 KB at 4; 3 waves:
+// 3.05 vs 2.83 ms user half, profiles/r05e/ab_k64_waves4_vs_3.log)
+constexpr int PS64_WAVES = 4;
 
 // Block LDL^T solve on the Gram tiles left in the MFMA accumulators (no LDS copy of the matrix).
 // With C = KP/16 the accumulators hold G' = P G P^T (feature f = C*i + b at position 16*b + i) as upper
@@ -713,8 +623,8 @@ __host__ __device__ constexpr int la_item_I(int C, int P, int t) {   // -1: the 
 // of each block; buf is KP floats of per-wave LDS.
 // Tile storage of the solve. Up to KP = 64 the tiles stay in the MFMA accumulator registers (RegTiles), and so do
 // they at KP = 128 on the pre-split path, which keeps no copy of the system (RowResidual); the other KP = 128 paths
-// (36 tiles = 144 registers per copy, plus the kept copy) hold the working tiles in per-wave LDS ([tile][lane][reg],
-// CFK_LDS_B128; or [tile][reg][lane]: conflict-free b32 accesses), loaded a tile at a time (LdsTiles).
+// (36 tiles = 144 registers per copy, plus the kept copy) hold the working tiles in per-wave LDS ([tile][lane][reg]),
+// loaded a tile at a time (LdsTiles).
 template <int C>
 struct RegTiles {
     f32x4* t;
@@ -728,28 +638,11 @@ struct RegStore {
     __device__ __forceinline__ void put(int i, const f32x4& v) { t[i] = v; }
 };
 // KP = 128 working tiles: [tile][lane][reg] so a tile moves with one ds_read_b128 / ds_write_b128 per lane
-// (kbench, k = 128: user half 23.3 -> 20.5 ms against the [tile][reg][lane] b32 layout, at the cost of 3 VGPR
-// spills); CFK_LDS_B128=0 restores the b32 layout
-#ifndef CFK_LDS_B128
-#define CFK_LDS_B128 1
-#endif
+// (kbench, k = 128: user half 23.3 -> 20.5 ms against a [tile][reg][lane] b32 layout, at the cost of 3 VGPR spills)
 struct LdsTiles {
-    float* p;   // per-wave base + lane (b32 layout [tile][reg][lane]) or + 4 * lane (b128 layout [tile][lane][reg])
-    __device__ __forceinline__ f32x4 get(int i) const {
-        if constexpr (CFK_LDS_B128) return *(const f32x4*)(p + i * 256);
-        f32x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = p[(i * 4 + r) * 64];
-        return v;
-    }
-    __device__ __forceinline__ void put(int i, const f32x4& v) {
-        if constexpr (CFK_LDS_B128) {
-            *(f32x4*)(p + i * 256) = v;
-            return;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) p[(i * 4 + r) * 64] = v[r];
-    }
+    float* p;   // per-wave base + 4 * lane
+    __device__ __forceinline__ f32x4 get(int i) const { return *(const f32x4*)(p + i * 256); }
+    __device__ __forceinline__ void put(int i, const f32x4& v) { *(f32x4*)(p + i * 256) = v; }
 };
 template <int C>
 constexpr bool tiles_in_lds() { return C > 4; }
@@ -776,11 +669,9 @@ struct RowResidual {
 // DUAL: the system is the entry Gram of a short row (als_solve_dual): unknown 16b + j = the row's entry at
 // physical position 16b + j, real when that entry exists (padding entries get an identity row), and the
 // solution alpha goes to buf[16b + j] (read by the caller after a wave_sync) instead of a factor row.
-// marks (debug build's pipelined-launch accounting, else null): shader clock after the scaling, the
-// factorisation, the first substitution, and at the end.
-template <int C, bool DUAL = false, bool FORCE_SWAP = false, class TT, class KT>
+template <int C, bool DUAL = false, class TT, class KT>
 __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc)[C], float* buf, const Task& tk,
-                                            const SolveArgs& a, int lane, uint64_t* marks = nullptr) {
+                                            const SolveArgs& a, int lane) {
     const int g = lane >> 4, j = lane & 15;
     float* out = (float*)a.out + factor_row(a.row_offset, a.rows_per_chunk, a.chunk_stride, tk.row) * (int64_t)(16 * C);
     auto is_real = [&](int b) { return DUAL ? logical_entry(16 * b + j) < tk.nent : C * j + b < a.k; };
@@ -852,14 +743,12 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 #pragma unroll
     for (int b = 0; b < C; ++b) b0[b] = col_sum(rhs_acc[b]) * scol[b];
 
-    if (marks) marks[0] = __builtin_amdgcn_s_memtime();
-    // ---- factorisation (matrix part only) ----
+    // ---- factorisation (matrix part only), lookahead schedule ----
     float nrd_min = -1.f;
-    constexpr bool SWAPC = FORCE_SWAP || 16 * C >= CFK_COL_SWAP;
-    if constexpr (CFK_SOLVE_LOOKAHEAD) {
+    {
         {
             f32x4 S0 = T.get(tile_index<C>(0, 0));
-            sweep_tile<SWAPC>(S0, lane, nrd_min);
+            sweep_tile(S0, lane, nrd_min);
             T.put(tile_index<C>(0, 0), S0);
         }
         static_for<0, C - 1>([&](auto P_) {
@@ -887,50 +776,12 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
             // the sweep of T_{P+1,P+1} with step P's remaining items between its 16 pivot steps
             static_for<0, 16>([&](auto Q_) {
                 constexpr int q = decltype(Q_)::value;
-                sweep_step<SWAPC, q>(D, lane, nrd_min);
+                sweep_step<q>(D, lane, nrd_min);
                 static_for<q * m / 16, (q + 1) * m / 16>(item);
             });
             T.put(tile_index<C>(P + 1, P + 1), D);
         });
-    } else
-    static_for<0, C>([&](auto P_) {
-        constexpr int P = decltype(P_)::value;
-        f32x4 S = T.get(tile_index<C>(P, P));
-        sweep_tile<SWAPC>(S, lane, nrd_min);
-        T.put(tile_index<C>(P, P), S);
-        // Block columns J in DESCENDING order: V'_PJ only updates T_IJ (P < I <= J) from the still-unreplaced
-        // T_PI (I <= J), so block row P can take V'_PJ right away and one V is live at a time. Every T_IJ
-        // receives the same single update per P as in any order: bitwise equal.
-        static_for<0, C - 1 - P>([&](auto Q_) {
-            constexpr int J = C - 1 - decltype(Q_)::value;
-            f32x4 TPJ = T.get(tile_index<C>(P, J));
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if constexpr (CFK_SOLVE_DRAIN) {
-                pin4(S);
-                pin4(TPJ);
-                pin4(v);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-#pragma unroll
-            for (int s = 0; s < 4; ++s) v = __builtin_amdgcn_mfma_f32_16x16x4f32(S[s], TPJ[s], v, 0, 0, 0);
-            if constexpr (CFK_SOLVE_DRAIN) MFMA_DRAIN();
-            static_for<P + 1, J + 1>([&](auto I_) {
-                constexpr int I = decltype(I_)::value;
-                f32x4 TPI = T.get(tile_index<C>(P, I));
-                f32x4 D = T.get(tile_index<C>(I, J));
-                if constexpr (CFK_SOLVE_DRAIN) {
-                    pin4(TPI);
-                    pin4(D);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-#pragma unroll
-                for (int s = 0; s < 4; ++s) D = __builtin_amdgcn_mfma_f32_16x16x4f32(TPI[s], v[s], D, 0, 0, 0);
-                if constexpr (CFK_SOLVE_DRAIN) MFMA_DRAIN();
-                T.put(tile_index<C>(I, J), D);
-            });
-            T.put(tile_index<C>(P, J), v);   // block row P now holds V'_PJ
-        });
-    });
+    }
 
     // ---- x = A^{-1} rhs with the factorisation ----
     auto solve_vec = [&](const float (&rhs)[C], float (&x)[C]) {
@@ -978,10 +829,8 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
             }
         });
     };
-    if (marks) marks[1] = __builtin_amdgcn_s_memtime();
     float x[C];
     solve_vec(b0, x);
-    if (marks) marks[2] = __builtin_amdgcn_s_memtime();
     // Well-conditioned systems skip the refinement step: every pivot of the scaled (unit-diagonal) system is a
     // Schur-complement diagonal in (0, 1]; when the smallest is >= a.refine_min_pivot the block factorisation's
     // error is already below the reference's own fp32 LU error. The test is wave-uniform.
@@ -990,7 +839,6 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 #pragma unroll
         for (int b = 0; b < C; ++b) xs[b] = x[b] * scol[b];
         emit(xs);
-        if (marks) marks[3] = __builtin_amdgcn_s_memtime();
         return;
     }
     if (a.flags & SOLVE_FLAG_SKIP_REFINE) {   // diagnostics only
@@ -1088,7 +936,6 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 #pragma unroll
     for (int b = 0; b < C; ++b) xs[b] = (x[b] + dx[b]) * scol[b];
     emit(xs);
-    if (marks) marks[3] = __builtin_amdgcn_s_memtime();
 }
 
 // Waves (tasks) per workgroup of the MFMA kernel: 4, or 2 at KP = 128, whose 72 KB of per-wave LDS tiles
@@ -1201,18 +1048,10 @@ __device__ __forceinline__ void store_partial(const SolveArgs& a, const Task& tk
 }
 
 // Pre-split fp16 Gram of one FULL / PARTIAL task into acc (tiles, RHS) and E (the diagonal tiles' h m^T terms,
-// folded by the caller), in the table's units. img: the wave's 2 C KB LDS image (1-KB aligned); buf: its KP floats.
-// NOE: E unused -- a diagonal tile takes hh + hm + mh like the others (3 MFMAs; 32 accumulator registers fewer at
-// KP = 128). RHS (0: the 2 C RHS MFMA tiles; 1 / 2: v_dot2_f32_f16 on the operand registers -- the lane's h/m pairs
-// of its 8 entries times the rh and rm pairs (1) or the rh pairs alone when every rating is exact in fp16 (2),
-// per-lane partial sums reduced over the 4 lane rows at the end): 2 C MFMAs per block fewer, 8 C or 4 C VALU more.
-// The pipelined KP = 128 Gram role, whose wave has half the register file, needs both (108 MFMAs per block).
-// DBUF: the LDS-DMA two blocks ahead into two images (img, img2), so a block's DMA has two blocks' MFMAs to land
-// under instead of one (the one-wave-per-SIMD KP = 128 launch, where no other wave covers the wait).
-template <int KP, bool NOE = false, int RHS = 0, bool DBUF = false>
+// folded by the caller), in true units. img: the wave's 2 C KB LDS image (1-KB aligned); buf: its KP floats.
+template <int KP>
 __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk, MfmaAcc<KP / 16>& acc,
-                                              f32x4 (&E)[KP / 16], unsigned char* img, float* buf, int lane,
-                                              unsigned char* img2 = nullptr) {
+                                              f32x4 (&E)[KP / 16], unsigned char* img, float* buf, int lane) {
     constexpr int C = KP / 16;
     using Acc = MfmaAcc<C>;
     constexpr int B = BLOCK_SUBSTEPS;
@@ -1229,24 +1068,18 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
     constexpr int NPL = 2;                 // planes h, m
     const char* tbase = (const char*)a.opp_split;
     const int sc = split_exp(*a.amax);     // the table's scale 2^sc (wave-uniform scalar load)
-    constexpr bool DOT2 = RHS != 0;
-    constexpr int NR = DOT2 ? 1 : C;       // RHS MFMA tiles (dot2 RHS: none)
-    f32x4 racc[NR];
+    f32x4 racc[C];
 #pragma unroll
-    for (int b = 0; b < NR; ++b) racc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float rsum[C];                         // dot2 RHS: per-lane partial sums
-#pragma unroll
-    for (int b = 0; b < C; ++b) rsum[b] = 0.f;
+    for (int b = 0; b < C; ++b) racc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
     // the block's MFMAs on operands P[plane h/m][feature block b] (entries 8g..8g+7 of feature C j + b as
-    // fp16 pairs) and the fp16 rating pairs R of the same entries (rh or rm by the lane's column; dot2 RHS: rh in
-    // R, rm in Rm, every lane)
-    auto mfma_block = [&](const u32x4 (&P)[NPL][C], const u32x4& R, const u32x4& Rm) {
+    // fp16 pairs) and the fp16 rating pairs R of the same entries (rh or rm by the lane's column)
+    auto mfma_block = [&](const u32x4 (&P)[NPL][C], const u32x4& R) {
 #pragma unroll
         for (int b1 = 0; b1 < C; ++b1)
 #pragma unroll
             for (int b2 = b1; b2 < C; ++b2) {
                 f32x4 t = acc.g[tile_index<C>(b1, b2)];
-                if (CFK_DIAG_SYM && !NOE && b1 == b2) {
+                if (b1 == b2) {
                     E[b1] = mfma_f16(P[0][b1], P[1][b1], E[b1]);
                 } else {
                     t = mfma_f16(P[0][b1], P[1][b2], t);
@@ -1255,29 +1088,12 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
                 t = mfma_f16(P[0][b1], P[0][b2], t);
                 acc.g[tile_index<C>(b1, b2)] = t;
             }
-        if constexpr (DOT2) {
 #pragma unroll
-            for (int b = 0; b < C; ++b) {
-                float v = rsum[b];
-#pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    if constexpr (RHS == 1) {
-                        v = dot2_f16(P[1][b][w], Rm[w], v);
-                        v = dot2_f16(P[0][b][w], Rm[w], v);
-                    }
-                    v = dot2_f16(P[1][b][w], R[w], v);
-                    v = dot2_f16(P[0][b][w], R[w], v);
-                }
-                rsum[b] = v;
-            }
-        } else {
-#pragma unroll
-            for (int b = 0; b < C; ++b) {
-                f32x4 t = racc[b];
-                t = mfma_f16(P[1][b], R, t);
-                t = mfma_f16(P[0][b], R, t);
-                racc[b] = t;
-            }
+        for (int b = 0; b < C; ++b) {
+            f32x4 t = racc[b];
+            t = mfma_f16(P[1][b], R, t);
+            t = mfma_f16(P[0][b], R, t);
+            racc[b] = t;
         }
         MFMA_DRAIN();
     };
@@ -1311,7 +1127,7 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
         tpl[x] = tbase + (x / NH) * 2 * KP + (x % NH) * 128;
         asm volatile("" : "+s"(tpl[x]));
     }
-    auto issue_to = [&](const i32x4& cv, unsigned char* im) {
+    auto issue = [&](const i32x4& cv) {
         static_for<0, 4>([&](auto M_) {
             constexpr int m = decltype(M_)::value;
             // 24-bit multiply: pre-split tables are host-checked < 2^24 rows and < 4 GiB
@@ -1319,88 +1135,39 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
             static_for<0, NPL * NH>([&](auto X_) {
                 constexpr int x = decltype(X_)::value;   // plane x / NH, half x % NH
                 __builtin_amdgcn_global_load_lds((const void*)(tpl[x] + vo),
-                                                 (lds_void*)(im + (x * 4 + m) * 1024), 16, 0, 0);
+                                                 (lds_void*)(img + (x * 4 + m) * 1024), 16, 0, 0);
             });
         });
     };
-    auto issue = [&](const i32x4& cv) { issue_to(cv, img); };
-    auto read1 = [&](auto PL_, auto B_, unsigned char* im) {
+    auto read1 = [&](auto PL_, auto B_) {
         constexpr int pl = decltype(PL_)::value, b = decltype(B_)::value;
         u32x4 P;
         static_for<0, 2>([&](auto H_) {
             constexpr int h = decltype(H_)::value;
             const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_s16x4*)(im + rd[b & 3] + ((pl * NH + (b >> 2)) * 4 + h) * 1024));
+                (lds_s16x4*)(img + rd[b & 3] + ((pl * NH + (b >> 2)) * 4 + h) * 1024));
             const u32x2 w = __builtin_bit_cast(u32x2, v);
             P[2 * h] = w[0];
             P[2 * h + 1] = w[1];
         });
         return P;
     };
-    auto read_from = [&](u32x4 (&P)[NPL][C], unsigned char* im) {
+    auto read = [&](u32x4 (&P)[NPL][C]) {
         static_for<0, NPL>([&](auto PL_) {
-            static_for<0, C>([&](auto B_) { P[decltype(PL_)::value][decltype(B_)::value] = read1(PL_, B_, im); });
+            static_for<0, C>([&](auto B_) { P[decltype(PL_)::value][decltype(B_)::value] = read1(PL_, B_); });
         });
     };
-    auto read = [&](u32x4 (&P)[NPL][C]) { read_from(P, img); };
-    if constexpr (DBUF) {
-        static_assert(RHS == 0, "double-buffered pre-split Gram: RHS MFMA tiles");
-        if (nblk > 0) {
-            const int lastb = nblk - 1;
-            const i32x4* cp = (const i32x4*)(a.col_ps + tk.begin) + r8;   // + 8 per block
-            const u32x4* rp = (const u32x4*)(a.rat_pk + (j >= 8 ? a.rat_lo_off : 0) + (tk.begin >> 1)) + g;
-            // Vector-memory ops per block, in order: its image's DMA (2 C instructions), the column indices of the
-            // block two ahead, the ratings of this block. Steady state at block b's wait: after DMA(b) come cv(b+2),
-            // R(b), then block b+1's DMA, cv(b+3), R(b+1) -- so vmcnt(2 C + 2) leaves exactly block b+1's ops in
-            // flight (DMA(b), cv(b+2) and R(b) done). Past the end the DMAs repeat the last block (same counts).
-            constexpr int AHEAD = NPL * NH * 4 + 2;
-            i32x4 cv0 = cp[0], cv1 = cp[8 * min(1, lastb)];
-            issue_to(cv0, img);
-            cv0 = cp[8 * min(2, lastb)];
-            u32x4 R0 = rp[0];
-            issue_to(cv1, img2);
-            cv1 = cp[8 * min(3, lastb)];
-            u32x4 R1 = rp[4 * min(1, lastb)];
-            static_assert(AHEAD == 18, "DBUF vmcnt below assumes 16 DMA instructions per block (KP = 128)");
-            for (int b = 0; b < nblk; b += 2) {
-                u32x4 P[NPL][C];
-                asm volatile("s_waitcnt vmcnt(18)" ::: "memory");   // DMA(b), cv(b+2), R(b) (tests/test_isa_guard.py)
-                read_from(P, img);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // operands in registers: the image is free
-                const u32x4 Ra = R0;
-                issue_to(cv0, img);                                  // DMA(b+2)
-                cv0 = cp[8 * min(b + 4, lastb)];
-                R0 = rp[4 * min(b + 2, lastb)];
-                __builtin_amdgcn_sched_barrier(0);
-                mfma_block(P, Ra, Ra);
-                __builtin_amdgcn_sched_barrier(0);
-                if (b + 1 > lastb) break;                             // wave-uniform
-                asm volatile("s_waitcnt vmcnt(18)" ::: "memory");   // DMA(b+1), cv(b+3), R(b+1)
-                read_from(P, img2);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                const u32x4 Rb = R1;
-                issue_to(cv1, img2);                                 // DMA(b+3)
-                cv1 = cp[8 * min(b + 5, lastb)];
-                R1 = rp[4 * min(b + 3, lastb)];
-                __builtin_amdgcn_sched_barrier(0);
-                mfma_block(P, Rb, Rb);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the DMAs issued past the last block have landed
-        }
-    } else if (nblk > 0) {
+    if (nblk > 0) {
         const int lastb = nblk - 1;
         const i32x4* cp = (const i32x4*)(a.col_ps + tk.begin) + r8;          // + 8 per block
-        // rating pairs of the lane's column half: rh (columns 0-7) or rm (columns 8-15); dot2 RHS: rh, rm in Rmn
-        const u32x4* rp = (const u32x4*)(a.rat_pk + ((j >= 8 && !DOT2) ? a.rat_lo_off : 0) + (tk.begin >> 1)) + g;
-        const u32x4* rpm = (const u32x4*)(a.rat_pk + a.rat_lo_off + (tk.begin >> 1)) + g;
+        // rating pairs of the lane's column half: rh (columns 0-7) or rm (columns 8-15)
+        const u32x4* rp = (const u32x4*)(a.rat_pk + (j >= 8 ? a.rat_lo_off : 0) + (tk.begin >> 1)) + g;
         i32x4 cv = cp[0];
-        u32x4 Rn = rp[0], Rmn = {0u, 0u, 0u, 0u};
-        if constexpr (RHS == 1) Rmn = rpm[0];
+        u32x4 Rn = rp[0];
         issue(cv);
         cv = cp[8 * min(1, lastb)];
         for (int b = 0; b < nblk; ++b) {
-            const u32x4 R = Rn, Rm = Rmn;
+            const u32x4 R = Rn;
             // every vector-memory op of this wave done: this block's LDS-DMA (and the column / rating loads
             // the DMA issue and the MFMAs below need anyway) -- explicit, not left to the compiler's tracking
             // of LDS-DMA writes (tests/test_isa_guard.py checks it)
@@ -1412,9 +1179,8 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
             if (b < lastb) issue(cv);
             cv = cp[8 * min(b + 2, lastb)];
             Rn = rp[4 * min(b + 1, lastb)];
-            if constexpr (RHS == 1) Rmn = rpm[4 * min(b + 1, lastb)];
             __builtin_amdgcn_sched_barrier(0);
-            mfma_block(P, R, Rm);
+            mfma_block(P, R);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -1423,26 +1189,16 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
     for (int t = 0; t < Acc::NT; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc.g[t][r] = ldexpf(acc.g[t][r], -2 * sc);
-    if constexpr (!NOE) {
 #pragma unroll
-        for (int b = 0; b < C; ++b)
+    for (int b = 0; b < C; ++b)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) E[b][r] = ldexpf(E[b][r], -2 * sc);
-    }
-    if constexpr (DOT2) {   // the other paths' per-lane RHS layout: the whole sum in row g = 0, zeros elsewhere
-#pragma unroll
-        for (int b = 0; b < C; ++b) {
-            const float v = ldexpf(col_sum(rsum[b]), -sc);
-            acc.rhs[b] = (g == 0) ? v : 0.f;
-        }
-        return;
-    }
+        for (int r = 0; r < 4; ++r) E[b][r] = ldexpf(E[b][r], -2 * sc);
     // RHS tiles (row i of block b = feature C i + b; column 0 = Y^T rh, column 8 = Y^T rm) -> the per-lane
     // partial layout of the other paths: lane (0, j) holds feature C j + b, the other rows zero (col_sum
     // restores it)
     wave_sync();
 #pragma unroll
-    for (int b = 0; b < NR; ++b) {
+    for (int b = 0; b < C; ++b) {
         f32x4 v = racc[b];
 #pragma unroll
         for (int r = 0; r < 4; ++r)   // lane (g, 8) += lane (g, 0): DPP row_shr:8
@@ -1460,8 +1216,7 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
 // gather kernel so neither carries the other's code and registers.
 // GRIDLOOP: a grid-stride loop over the tasks (the range guard's fallback launch, whose grid is capped: when the
 // pre-split serves the half, as it nearly always does, its waves exit without a full-size grid's dispatch cost).
-template <int KP, int MINW, bool SPLIT, bool PRESPLIT = false, bool REDUCE = false, bool NOE = false, int RHS = 0,
-          bool GRIDLOOP = false, bool DBUF = false>
+template <int KP, int MINW, bool SPLIT, bool PRESPLIT = false, bool REDUCE = false, bool GRIDLOOP = false>
 __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(SolveArgs a) {
     constexpr int C = KP / 16;
     constexpr int NW = mfma_waves<KP>();
@@ -1478,9 +1233,6 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
     constexpr int STAGE = (PRESPLIT && !REDUCE) ? 2 * C * 1024 : 16;
     __shared__ __attribute__((aligned(1024))) unsigned char stage_lds[NW][STAGE];
     (void)stage_lds;
-    // DBUF: the second image per wave, a separate LDS object
-    __shared__ __attribute__((aligned(1024))) unsigned char stage_lds2[NW][DBUF ? STAGE : 16];
-    (void)stage_lds2;
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // the table-range guard (presplit_ok): a pre-split launch serves the half only in range, its guarded on-the-fly
@@ -1574,7 +1326,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                 for (int c = 0; c < C; ++c) acc.rhs[c] += r * y[c];
             };
             if constexpr (PRESPLIT) {
-                gram_presplit<KP, NOE, RHS, DBUF>(a, tk, acc, E, stage_lds[uni(wave)], buf, lane, stage_lds2[uni(wave)]);
+                gram_presplit<KP>(a, tk, acc, E, stage_lds[uni(wave)], buf, lane);
             } else if constexpr (SPLIT) {
                 // Split-bf16 Gram: one v_mfma_f32_16x16x32_bf16 consumes a whole 32-entry block. Lane (g, j)
                 // holds A[i = j][k = 8g + t] = y_t[C*j + b] (its own gathered piece, component b, entry t of its
@@ -1615,14 +1367,13 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                             M[b][q] = m;
                             L[b][q] = l;
                         }
-                    if constexpr (CFK_RHS_EARLY) {
+                    // the RHS before the MFMA group, materialised (see the RHS note at MFMA_DRAIN)
 #pragma unroll
-                        for (int t = 0; t < B; ++t)
+                    for (int t = 0; t < B; ++t)
 #pragma unroll
-                            for (int c = 0; c < C; ++c) acc.rhs[c] += x.r[t >> 2][t & 3] * y[t][c];
+                        for (int c = 0; c < C; ++c) acc.rhs[c] += x.r[t >> 2][t & 3] * y[t][c];
 #pragma unroll
-                        for (int c = 0; c < C; ++c) pin(acc.rhs[c]);
-                    }
+                    for (int c = 0; c < C; ++c) pin(acc.rhs[c]);
                     // the operands are materialised above (pin: MachineSink ignores sched_barrier), so the MFMA group
                     // below contains no VALU that could overwrite an operand register of an MFMA in flight
                     __builtin_amdgcn_sched_barrier(0);
@@ -1632,7 +1383,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                         for (int b2 = b1; b2 < C; ++b2) {
                             f32x4 t = acc.g[tile_index<C>(b1, b2)];
                             t = mfma_k32(M[b1], M[b2], t);
-                            if (CFK_DIAG_SYM && b1 == b2) {
+                            if (b1 == b2) {
                                 f32x4 e = E[b1];
                                 e = mfma_k32(H[b1], L[b1], e);
                                 e = mfma_k32(H[b1], M[b1], e);
@@ -1647,17 +1398,11 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                             acc.g[tile_index<C>(b1, b2)] = t;
                         }
                     MFMA_DRAIN();
-                    if constexpr (!CFK_RHS_EARLY) {
-#pragma unroll
-                        for (int t = 0; t < B; ++t)
-#pragma unroll
-                            for (int c = 0; c < C; ++c) acc.rhs[c] += x.r[t >> 2][t & 3] * y[t][c];
-                    }
                 };
                 // Two blocks per trip with ping-pong buffers (no register rotation): column indices are loaded two
                 // blocks ahead of their gathers' use, gathers and ratings one block ahead of their MFMAs.
                 // Invariant at the loop top: Y0/R0 in flight for block b, I1 = columns of b+1, I0 = columns of b+2.
-                if (C > 4 && CFK_K128_INTERLEAVE && nblk > 0) {
+                if (C > 4 && nblk > 0) {
                     // KP = 128, one wave per SIMD: no second wave hides the split VALU behind this wave's MFMAs, so
                     // the wave interleaves them itself. The tiles are issued column by column (column c = tiles
                     // (b1 <= c, c): 6c + 4 MFMAs), and the split of feature block c + 1 -- the only new operand
@@ -1696,7 +1441,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                             for (int b1 = 0; b1 <= c; ++b1) {
                                 f32x4 t = acc.g[tile_index<C>(b1, c)];
                                 t = mfma_k32(M[b1], M[c], t);
-                                if (CFK_DIAG_SYM && b1 == c) {
+                                if (b1 == c) {
                                     f32x4 e = E[b1];
                                     e = mfma_k32(H[b1], L[b1], e);
                                     e = mfma_k32(H[b1], M[b1], e);
@@ -1754,43 +1499,6 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                         R0 = R1;
                     }
                     block(Y0, R0, Y1, No{});
-                } else if (C > 4 && nblk > 0) {
-                    // KP = 128 (1 wave per SIMD, 144 accumulator registers): one staging set, rotated
-                    Cols Ic, In;
-                    Rats Rc, Rn;
-                    VT Yc[B], Yn[B];
-                    const int lastb = nblk - 1;
-                    load_cols(0, Ic);
-                    load_cols(min(1, lastb), In);
-                    gather_blk(Ic, Yc);
-                    load_rats(0, Rc);
-                    for (int b = 0; b < lastb; ++b) {
-                        gather_blk(In, Yn);
-                        load_rats(b + 1, Rn);
-                        load_cols(min(b + 2, lastb), In);
-                        __builtin_amdgcn_sched_barrier(0);
-                        split_step(Yc, Rc);
-                        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                        for (int t = 0; t < B; ++t) Yc[t] = Yn[t];
-                        Rc = Rn;
-                    }
-                    split_step(Yc, Rc);
-                } else if (MINW >= 3 && nblk > 0) {
-                    // three waves per SIMD: one gather buffer, columns one block ahead
-                    Cols I;
-                    Rats R;
-                    VT Y[B];
-                    const int lastb = nblk - 1;
-                    load_cols(0, I);
-                    for (int b = 0; b < nblk; ++b) {
-                        gather_blk(I, Y);
-                        load_rats(b, R);
-                        load_cols(min(b + 1, lastb), I);
-                        __builtin_amdgcn_sched_barrier(0);
-                        split_step(Y, R);
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
                 } else if (nblk > 0) {
                     Cols I0, I1;
                     Rats R0, R1;
@@ -1902,20 +1610,17 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             }
         }
 
-        if constexpr (SPLIT && CFK_DIAG_SYM && !NOE) {
-            if constexpr (!REDUCE) {
-                if constexpr (PRESPLIT && CFK_FOLD_LDS)
-                    fold_diag_lds<C>(acc, E, lane, stage_lds[uni(wave)]);   // the image is free after the Gram
-                else
-                    fold_diag<C>(acc, E, lane);
-            }
+        if constexpr (SPLIT && !REDUCE) {
+            if constexpr (PRESPLIT)
+                fold_diag_lds<C>(acc, E, lane, stage_lds[uni(wave)]);   // the image is free after the Gram
+            else
+                fold_diag<C>(acc, E, lane);
         }
 
         if (!REDUCE && tk.kind == TASK_PARTIAL) {
             store_partial<C>(a, tk, acc, lane);
             return;
         }
-
         if (a.flags & SOLVE_FLAG_SKIP_SOLVE) {   // diagnostics (kbench): Gram only
             float* out = (float*)a.out + factor_row(a.row_offset, a.rows_per_chunk, a.chunk_stride, tk.row) * (int64_t)KP;
             if (lane < 16) {
@@ -1925,7 +1630,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
             return;
         }
         if constexpr (TILES_LDS) {
-            LdsTiles T{tiles_lds[wave] + (CFK_LDS_B128 ? 4 : 1) * lane};
+            LdsTiles T{tiles_lds[wave] + 4 * lane};
             RegStore<C> A0;
 #pragma unroll
             for (int p = 0; p < Acc::NT; ++p) T.put(p, acc.g[p]);
@@ -1946,308 +1651,6 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
         const int tid = blockIdx.x * NW + wave;
         if (tid < a.n_tasks) task(tid);
     }
-}
-
-// ---------------------------------------------------------------------------------------------------
-// Pipelined pre-split launch: Gram waves hand finished systems to solver waves through LDS
-// ---------------------------------------------------------------------------------------------------
-// One persistent workgroup per CU with NG Gram waves and NS solver waves (the hot path of the k = 64 user half and
-// of both halves at k = 128). Waves 0..NG-1 take FULL / PARTIAL tasks from a device queue (one vector atomic per
-// task on a.queue, zeroed before the launch; tasks stay longest first) and run the pre-split Gram (gram_presplit);
-// a PARTIAL task stores its partial slot as in als_solve_mfma, a FULL task's Gram tiles (accumulator layout,
-// [tile][lane][4]), RHS and task index go to a free hand-off slot in LDS. Waves NG.. take filled slots and run the
-// tile solve (solve_tiles with RowResidual) and store the factor row: the same arithmetic in the same order as
-// als_solve_mfma<KP, W, true, true>, so bitwise-equal results. The roles never hold each other's state, so each
-// fits its share of the register file -- at KP = 128 two waves per SIMD (one Gram, one solver) instead of the
-// one-kernel path's single wave holding both -- and the solve's latency-bound pivot chains run beside the Gram's
-// gathers and MFMAs instead of after them.
-// Slot protocol (LDS, workgroup scope): FREE -(Gram CAS)-> WRITING -(release store)-> FULL -(solver CAS)->
-// READING -(release store once its reads are in registers)-> FREE. A Gram wave waits only for a FREE slot, a
-// solver only for a FULL slot or the end (all Gram waves counted done, each after its last publish): no wait
-// cycle. Every wait is bounded in time (PC_WAIT_TICKS of the 100 MHz real-time counter); a wave that runs out
-// records it in the integrity record (slot PC_TIMEOUT_SLOT) and leaves, so the grid always drains.
-constexpr int PC_FREE = 0, PC_WRITING = 1, PC_FULL = 2, PC_READING = 3;
-// debug build: shader-clock accounting of the roles (a.pc_stats); product build: nothing
-#ifdef CFK_DEBUG_KNOBS
-#define PC_CLOCK() __builtin_amdgcn_s_memtime()
-#else
-#define PC_CLOCK() 0ull
-#endif
-__device__ __forceinline__ void pc_stats_add(const SolveArgs& a, int i0, uint64_t v0, int i1, uint64_t v1, int i2,
-                                             uint64_t v2, int lane) {
-#ifdef CFK_DEBUG_KNOBS
-    if (a.pc_stats && lane == 0) {
-        atomicAdd(a.pc_stats + i0, (unsigned long long)v0);
-        atomicAdd(a.pc_stats + i1, (unsigned long long)v1);
-        atomicAdd(a.pc_stats + i2, (unsigned long long)v2);
-    }
-#else
-    (void)a; (void)i0; (void)v0; (void)i1; (void)v1; (void)i2; (void)v2; (void)lane;
-#endif
-}
-constexpr uint64_t PC_WAIT_TICKS = 200000000ull;   // 2 s
-__device__ __forceinline__ uint64_t pc_now() { return __builtin_amdgcn_s_memrealtime(); }
-
-// LDS of the pipelined launch: dynamic (pc_smem), so that the solver role -- a separate, not inlined function --
-// addresses the same LDS objects as the kernel: per Gram wave a 2 C KB LDS-DMA image, per wave KP floats of solve
-// scratch, NSLOT hand-off slots (Gram tiles [tile][lane][4], RHS [16 C], task index), the slot states, the
-// count of finished Gram waves.
-extern __shared__ __attribute__((aligned(1024))) unsigned char pc_smem[];
-template <int KP, int NG, int NS, int NSLOT>
-struct PcLds {
-    static constexpr int C = KP / 16;
-    static constexpr int NT = MfmaAcc<C>::NT;
-    static constexpr int IMG_BYTES = 2 * C * 1024;
-    static constexpr int SBUF_OFF = NG * IMG_BYTES;
-    static constexpr int SLOT_OFF = SBUF_OFF + (NG + NS) * KP * 4;
-    static constexpr int SLOT_BYTES = NT * 1024 + 16 * C * 4 + 16;   // tiles, RHS, task index (+ pad)
-    static constexpr int STATE_OFF = SLOT_OFF + NSLOT * SLOT_BYTES;
-    static constexpr int BYTES = STATE_OFF + 4 * (NSLOT + 1);         // + ndone
-    static_assert(BYTES <= 160 * 1024, "pipelined launch: LDS");
-    static __device__ __forceinline__ unsigned char* img(int w) { return pc_smem + w * IMG_BYTES; }
-    static __device__ __forceinline__ float* sbuf(int w) { return (float*)(pc_smem + SBUF_OFF + w * KP * 4); }
-    static __device__ __forceinline__ float* slot(int i) { return (float*)(pc_smem + SLOT_OFF + i * SLOT_BYTES); }
-    static __device__ __forceinline__ int* state() { return (int*)(pc_smem + STATE_OFF); }
-};
-
-// The launch's arguments as wave-uniform values (readfirstlane of every field): inside a called function they
-// arrive in memory/VGPRs, and the solve branches on them and forms its addresses from them.
-__device__ __forceinline__ int64_t uni64(int64_t v) {
-    return ((int64_t)uni((int)(v >> 32)) << 32) | (int64_t)(uint32_t)uni((int)(uint32_t)v);
-}
-template <class P>
-__device__ __forceinline__ P unip(P v) { return (P)uni64((int64_t)(uintptr_t)v); }
-__device__ __forceinline__ float unif(float v) { return __int_as_float(uni(__float_as_int(v))); }
-__device__ __forceinline__ SolveArgs uniform_args(const SolveArgs& in) {
-    SolveArgs a = in;
-    a.tasks = unip(in.tasks);
-    a.n_tasks = uni(in.n_tasks);
-    a.k = uni(in.k);
-    a.col = unip(in.col);
-    a.rat = unip(in.rat);
-    a.opp = unip(in.opp);
-    a.out = unip(in.out);
-    a.row_offset = uni64(in.row_offset);
-    a.partials = unip(in.partials);
-    a.lambda = unif(in.lambda);
-    a.sentinel = uni(in.sentinel);
-    a.flags = uni(in.flags);
-    a.opp_split = unip(in.opp_split);
-    a.gen = (uint32_t)uni((int)in.gen);
-    a.integrity = unip(in.integrity);
-    a.refine_min_pivot = unif(in.refine_min_pivot);
-    a.rat_pk = unip(in.rat_pk);
-    a.col_ps = unip(in.col_ps);
-    a.rows_per_chunk = uni(in.rows_per_chunk);
-    a.chunk_stride = uni64(in.chunk_stride);
-    a.rat_lo_off = uni64(in.rat_lo_off);
-    a.amax = unip(in.amax);
-    a.scratch_slabs = uni64(in.scratch_slabs);
-    a.queue = unip(in.queue);
-    a.pc_stats = unip(in.pc_stats);
-    a.extra_lds = uni(in.extra_lds);
-    return a;
-}
-
-// Solver role of als_solve_pc: one filled hand-off slot -> registers (then the slot is released) -> tile solve ->
-// factor row. Not inlined: as a call, the solve's registers are allocated for the solve alone; inlined into the
-// persistent loop the allocator kept loop-wide values live through it and spilled ~100 VGPRs at KP = 128.
-template <int KP, int NG, int NS, int NSLOT>
-__device__ __attribute__((noinline)) void pc_solve_slot(SolveArgs a_in, int sl_in, int wave_in) {
-    using L = PcLds<KP, NG, NS, NSLOT>;
-    constexpr int C = KP / 16;
-    using Acc = MfmaAcc<C>;
-#ifdef CFK_DEBUG_KNOBS
-    const uint64_t c_in = __builtin_amdgcn_s_memtime();
-#endif
-    const SolveArgs a = uniform_args(a_in);
-    const int sl = uni(sl_in), wave = uni(wave_in);
-    const int lane = __lane_id(), g = lane >> 4, j = lane & 15;
-    const float* sp = L::slot(sl);
-    Acc acc;
-#pragma unroll
-    for (int p = 0; p < Acc::NT; ++p) acc.g[p] = *(const f32x4*)(sp + p * 256 + 4 * lane);
-#pragma unroll
-    for (int b = 0; b < C; ++b) acc.rhs[b] = (g == 0) ? sp[Acc::NT * 256 + 16 * b + j] : 0.f;
-    const int t = uni(((const int*)sp)[Acc::NT * 256 + 16 * C]);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot is in registers: release it
-    if (lane == 0) __hip_atomic_store(L::state() + sl, PC_FREE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const Task tk = load_task(a.tasks + t);
-    if (a.flags & SOLVE_FLAG_SKIP_SOLVE) {   // diagnostics (kbench): Gram only
-        float* out = (float*)a.out + factor_row(a.row_offset, a.rows_per_chunk, a.chunk_stride, tk.row) * (int64_t)KP;
-        if (lane < 16) {
-#pragma unroll
-            for (int b = 0; b < C; ++b) out[C * lane + b] = acc.g[tile_index<C>(b, b)][0] + acc.rhs[b];
-        }
-        return;
-    }
-    RegTiles<C> T{acc.g};
-    RowResidual A0;
-#ifdef CFK_DEBUG_KNOBS
-    uint64_t mk[4] = {c_in, c_in, c_in, c_in};
-    const uint64_t c_pre = __builtin_amdgcn_s_memtime();
-    solve_tiles<C, false, CFK_PC_SWAP != 0>(T, A0, acc.rhs, L::sbuf(wave), tk, a, lane, mk);
-    // setup (args, slot, task), scaling, factorisation, substitution, emit / refinement
-    if (a.pc_stats && lane == 0) {
-        atomicAdd(a.pc_stats + PC_STAT_T_SETUP, (unsigned long long)(c_pre - c_in));
-        atomicAdd(a.pc_stats + PC_STAT_T_SCALE, (unsigned long long)(mk[0] - c_pre));
-        atomicAdd(a.pc_stats + PC_STAT_T_FACTOR, (unsigned long long)(mk[1] - mk[0]));
-        atomicAdd(a.pc_stats + PC_STAT_T_SUBST, (unsigned long long)(mk[2] - mk[1]));
-        atomicAdd(a.pc_stats + PC_STAT_T_END, (unsigned long long)(mk[3] - mk[2]));
-    }
-#else
-    solve_tiles<C, false, CFK_PC_SWAP != 0>(T, A0, acc.rhs, L::sbuf(wave), tk, a, lane);
-#endif
-}
-
-template <int KP, int NG, int NS, int NSLOT>
-__global__ __launch_bounds__(64 * (NG + NS), 1) void als_solve_pc(SolveArgs a) {
-    using L = PcLds<KP, NG, NS, NSLOT>;
-    constexpr int C = KP / 16;
-    using Acc = MfmaAcc<C>;
-    constexpr auto WG = __HIP_MEMORY_SCOPE_WORKGROUP;
-    int* state = L::state();
-    int* ndone = state + NSLOT;
-
-    const int wave = uni((int)(threadIdx.x >> 6)), lane0 = threadIdx.x & 63;
-    if (!presplit_ok(a.amax)) return;   // out of the pre-split's range: the guarded fallback launch solves the half
-    if (threadIdx.x < NSLOT) state[threadIdx.x] = PC_FREE;
-    if (threadIdx.x == 0) *ndone = 0;
-    __syncthreads();   // the only workgroup barrier: every wave passes it before any wave waits on another
-
-#if defined(CFK_PC_ROLE_TEST) && CFK_PC_ROLE_TEST == 2
-    if (wave < NG) return;
-#endif
-    if (wave < NG) {
-        // ---- Gram role ----
-        unsigned char* img = L::img(wave);
-        float* buf = L::sbuf(wave);
-        uint64_t st_gram = 0, st_wait = 0, st_tasks = 0;   // debug-build cycle accounting (PC_CLOCK)
-        // task stream x = the workgroup's XCD (workgroups are dealt to the 8 XCDs round-robin): tasks x, x + 8, ...
-        // (still longest first), taken PC_CHUNK stream positions per vector atomic on the stream's own counter --
-        // one same-address atomic per task serialised the k = 64 user half at ~75 M atomics/s (5.1 ms)
-        const int x = (int)(blockIdx.x % PC_STREAMS);
-        int* qx = a.queue + x * PC_QSTRIDE;
-        const int nx = a.n_tasks > x ? (a.n_tasks - x + PC_STREAMS - 1) / PC_STREAMS : 0;
-        int pos = 0, end = 0;   // the wave's current chunk of stream positions
-        while (true) {
-            if (pos == end) {
-                int b = 0;
-                if (lane0 == 0) b = atomicAdd(qx, PC_CHUNK);
-                pos = uni(b);
-                end = pos + PC_CHUNK;
-            }
-            if (pos >= nx) break;
-            const int t = x + PC_STREAMS * pos++;
-            const uint64_t c0 = PC_CLOCK();
-            // a fresh lane id per task: nothing lane-derived is hoisted out of the loop and kept live across it
-            const int lane = opaque(lane0);
-            const Task tk = load_task(a.tasks + t);
-            Acc acc;
-#pragma unroll
-            for (int p = 0; p < Acc::NT; ++p) acc.g[p] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int c = 0; c < C; ++c) acc.rhs[c] = 0.f;
-            f32x4 E[C];
-#pragma unroll
-            for (int c = 0; c < C; ++c) E[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-            constexpr bool NOE = KP == 128;   // the KP = 128 Gram role fits its half of the register file so
-            constexpr int RHS = KP == 128 ? 1 : 0;   // (rh and rm pairs: one instantiation per role layout)
-            gram_presplit<KP, NOE, RHS>(a, tk, acc, E, img, buf, lane);
-            if constexpr (CFK_DIAG_SYM && !NOE) fold_diag<C>(acc, E, lane);
-            const uint64_t c1 = PC_CLOCK();
-            st_gram += c1 - c0;
-            ++st_tasks;
-            if (tk.kind == TASK_PARTIAL) {
-                store_partial<C>(a, tk, acc, lane);
-            } else {
-                // claim a FREE slot
-                int sl = -1;
-                const uint64_t t0 = pc_now();
-                while (true) {
-                    int cl = -1;
-                    if (lane == 0) {
-                        for (int i = 0; i < NSLOT; ++i) {
-                            int expct = PC_FREE;
-                            if (__hip_atomic_load(&state[i], __ATOMIC_RELAXED, WG) == PC_FREE &&
-                                __hip_atomic_compare_exchange_strong(&state[i], &expct, PC_WRITING, __ATOMIC_ACQUIRE,
-                                                                     __ATOMIC_RELAXED, WG)) {
-                                cl = i;
-                                break;
-                            }
-                        }
-                    }
-                    sl = uni(cl);
-                    if (sl >= 0 || pc_now() - t0 > PC_WAIT_TICKS) break;
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                st_wait += PC_CLOCK() - c1;
-                if (sl < 0) {   // no solver freed a slot in PC_WAIT_TICKS: record and leave (the grid drains)
-                    report_bad_slot(a.integrity, a.gen, PC_TIMEOUT_SLOT, tk.row, true, lane);
-                    break;
-                }
-                float* sp = L::slot(sl);
-#pragma unroll
-                for (int p = 0; p < Acc::NT; ++p) *(f32x4*)(sp + p * 256 + 4 * lane) = acc.g[p];
-                const int g = lane >> 4, j = lane & 15;
-                if (g == 0) {
-#pragma unroll
-                    for (int b = 0; b < C; ++b) sp[Acc::NT * 256 + 16 * b + j] = acc.rhs[b];
-                }
-                if (lane == 0) {
-                    ((int*)sp)[Acc::NT * 256 + 16 * C] = t;
-                    __hip_atomic_store(&state[sl], PC_FULL, __ATOMIC_RELEASE, WG);
-                }
-            }
-        }
-        if (lane0 == 0) __hip_atomic_fetch_add(ndone, 1, __ATOMIC_RELEASE, WG);
-        pc_stats_add(a, PC_STAT_GRAM, st_gram, PC_STAT_GRAM_WAIT, st_wait, PC_STAT_TASKS, st_tasks, lane0);
-        return;
-    }
-
-    // ---- solver role ----
-#if defined(CFK_PC_ROLE_TEST) && CFK_PC_ROLE_TEST == 1
-    return;
-#endif
-    // the solve is a latency-bound chain beside a Gram wave with independent MFMAs to spare: it issues first
-    if constexpr (CFK_PC_PRIO > 0) __builtin_amdgcn_s_setprio(CFK_PC_PRIO);
-    uint64_t t0 = pc_now();
-    uint64_t st_solve = 0, st_idle = 0, st_n = 0, c_idle = PC_CLOCK();
-    while (true) {
-        int cl = -1, fin = 0;
-        if (lane0 == 0) {
-            const int nd = __hip_atomic_load(ndone, __ATOMIC_ACQUIRE, WG);   // before the scan: see the publishes
-            for (int i = 0; i < NSLOT; ++i) {
-                int expct = PC_FULL;
-                if (__hip_atomic_load(&state[i], __ATOMIC_RELAXED, WG) == PC_FULL &&
-                    __hip_atomic_compare_exchange_strong(&state[i], &expct, PC_READING, __ATOMIC_ACQUIRE,
-                                                         __ATOMIC_RELAXED, WG)) {
-                    cl = i;
-                    break;
-                }
-            }
-            fin = cl < 0 && nd == NG;
-        }
-        const int sl = uni(cl);
-        if (uni(fin)) break;
-        if (sl < 0) {
-            if (pc_now() - t0 > PC_WAIT_TICKS) {   // no Gram wave published or finished in PC_WAIT_TICKS
-                report_bad_slot(a.integrity, a.gen, PC_TIMEOUT_SLOT, -1, true, lane0);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-        }
-        const uint64_t c0 = PC_CLOCK();
-        st_idle += c0 - c_idle;
-        pc_solve_slot<KP, NG, NS, NSLOT>(a, sl, wave);
-        c_idle = PC_CLOCK();
-        st_solve += c_idle - c0;
-        ++st_n;
-        t0 = pc_now();
-    }
-    st_idle += PC_CLOCK() - c_idle;
-    pc_stats_add(a, PC_STAT_SOLVE, st_solve, PC_STAT_SOLVE_IDLE, st_idle, PC_STAT_SOLVES, st_n, lane0);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -2337,7 +1740,7 @@ __global__ __launch_bounds__(64 * WAVES, CD <= 4 ? 2 : 1) void als_solve_dual(So
 #pragma unroll
     for (int b = 0; b < CD; ++b) rhs[b] = g == 0 ? rr[b] : 0.f;
     if constexpr (tiles_in_lds<CD>()) {   // CD = 6: 21 working tiles in per-wave LDS, as the KP = 128 primal solve
-        LdsTiles T{tiles_lds[wave] + (CFK_LDS_B128 ? 4 : 1) * lane};
+        LdsTiles T{tiles_lds[wave] + 4 * lane};
         RegStore<CD> A0;
 #pragma unroll
         for (int p = 0; p < Acc::NT; ++p) T.put(p, acc[p]);
@@ -2767,19 +2170,10 @@ hipError_t launch_solve_t(const SolveArgs& a, hipStream_t s, bool reduce) {
             als_solve_mfma<KP, MINW, false, false, true><<<grid, 64 * nw, 0, s>>>(a);
         } else if constexpr (!PRESPLIT && SPLIT) {
             if (a.presplit_fallback)   // the range guard's fallback: grid-stride over a capped grid
-                als_solve_mfma<KP, MINW, true, false, false, false, 0, true>
+                als_solve_mfma<KP, MINW, true, false, false, true>
                     <<<std::min<unsigned>(grid, (unsigned)std::max(1, a.grid_cap)), 64 * nw, dyn, s>>>(a);
             else
                 als_solve_mfma<KP, MINW, true, false><<<grid, 64 * nw, dyn, s>>>(a);
-        } else if constexpr (PRESPLIT && CFK_PS_DOT2) {   // RHS by dot2 (on the rh pairs alone when exact)
-            if (a.rat_exact16)
-                als_solve_mfma<KP, MINW, SPLIT, PRESPLIT, false, false, 2><<<grid, 64 * nw, dyn, s>>>(a);
-            else
-                als_solve_mfma<KP, MINW, SPLIT, PRESPLIT, false, false, 1><<<grid, 64 * nw, dyn, s>>>(a);
-        } else if constexpr (PRESPLIT && KP == 128 && CFK_PS128_DBUF) {
-            // the second image's column / rating registers: the diagonal tiles take hh + hm + mh (NOE) so the
-            // Gram keeps no register copies inside its MFMA groups (tests/test_isa_guard.py)
-            als_solve_mfma<KP, MINW, SPLIT, PRESPLIT, false, true, 0, false, true><<<grid, 64 * nw, dyn, s>>>(a);
         } else {
             als_solve_mfma<KP, MINW, SPLIT, PRESPLIT><<<grid, 64 * nw, dyn, s>>>(a);
         }
@@ -2799,6 +2193,26 @@ hipError_t launch_sq_t(const SqErrArgs& a, hipStream_t s) {
 }
 
 }  // namespace
+
+// dst block i <- src block perm[i]: 32 columns + 32 ratings per block, one 64-lane wave per block (16 B per lane)
+__global__ __launch_bounds__(256) void als_permute_blocks(const int32_t* __restrict__ col, const float* __restrict__ rat,
+                                                         int32_t* __restrict__ col_out, float* __restrict__ rat_out,
+                                                         const int32_t* __restrict__ perm, int64_t n_blocks) {
+    const int64_t blk = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (blk >= n_blocks) return;
+    const int l = threadIdx.x & 63;
+    const int64_t src = (int64_t)perm[blk] * BLOCK_ENTRIES;
+    const int64_t dst = blk * BLOCK_ENTRIES;
+    if (l < 8) ((u32x4*)(col_out + dst))[l] = ((const u32x4*)(col + src))[l];
+    else if (l < 16) ((u32x4*)(rat_out + dst))[l - 8] = ((const u32x4*)(rat + src))[l - 8];
+}
+hipError_t launch_permute_blocks(const int32_t* col, const float* rat, int32_t* col_out, float* rat_out,
+                                 const int32_t* perm, int64_t n_blocks, hipStream_t s) {
+    if (n_blocks <= 0) return hipSuccess;
+    als_permute_blocks<<<(unsigned)((n_blocks + 3) / 4), 256, 0, s>>>(col, rat, col_out, rat_out, perm, n_blocks);
+    return hipGetLastError();
+}
+
 
 bool variant_available(int precision, int kp, Path path) {
     if (path == Path::GENERIC) return kp % 16 == 0 && kp <= 1024;
@@ -2911,31 +2325,6 @@ hipError_t launch_pack_cols_ps(const int32_t* col, int32_t* dst, int64_t n_entri
     return hipGetLastError();
 }
 
-template <int KP, int NG, int NS, int NSLOT>
-hipError_t launch_pc_t(const SolveArgs& a, int cu_count, hipStream_t s) {
-    using L = PcLds<KP, NG, NS, NSLOT>;
-    hipError_t e = ensure_dyn_lds((const void*)als_solve_pc<KP, NG, NS, NSLOT>, L::BYTES);
-    if (e != hipSuccess) return e;
-    const unsigned grid = (unsigned)std::min<int64_t>(cu_count, ((int64_t)a.n_tasks + NG - 1) / NG);
-    als_solve_pc<KP, NG, NS, NSLOT><<<grid, 64 * (NG + NS), L::BYTES, s>>>(a);
-    return hipGetLastError();
-}
-// Pipelined pre-split launch (als_solve_pc): grid = min(CUs, enough workgroups for the tasks); a.queue zeroed here.
-hipError_t launch_solve_pc(int kp, const SolveArgs& a, int cu_count, hipStream_t s) {
-    if (a.n_tasks <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(a.queue, 0, PC_QUEUE_INTS * sizeof(int), s);
-    if (e != hipSuccess) return e;
-    if (kp == 64) {
-        constexpr int NG = CFK_PC64_NG, NS = 16 - CFK_PC64_NG;
-        return launch_pc_t<64, NG, NS, 4>(a, cu_count, s);
-    } else if (kp == 128) {
-        return launch_pc_t<128, 4, 4, 2>(a, cu_count, s);
-    } else {
-        return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
 hipError_t launch_dual(int kp, int cd, const SolveArgs& a, hipStream_t s) {
     if (a.n_tasks <= 0) return hipSuccess;
     const unsigned grid = (unsigned)blocks_for(a.n_tasks);
@@ -2951,7 +2340,7 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
                         bool reduce) {
     if (path == Path::GENERIC) return reduce ? hipErrorInvalidValue : launch_generic(precision, kp, a, s);
     if (precision == 0) {
-        // occupancy (waves per SIMD) per variant: KP <= 64 two, the pre-split KP = 64 Gram four (CFK_PS64_WAVES),
+        // occupancy (waves per SIMD) per variant: KP <= 64 two, the pre-split KP = 64 Gram four (PS64_WAVES),
         // KP = 128 one
         if (path == Path::MFMA) {
             if (kp == 32) return launch_solve_t<float, 32, Path::MFMA, 2>(a, s, reduce);
@@ -2959,7 +2348,7 @@ hipError_t launch_solve(int precision, int kp, Path path, const SolveArgs& a, hi
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA, 1>(a, s, reduce);
         } else if (path == Path::MFMA_SPLIT) {
             if (kp == 32) return launch_solve_t<float, 32, Path::MFMA_SPLIT, 2>(a, s, reduce);
-            if (kp == 64 && presplit) return launch_solve_t<float, 64, Path::MFMA_SPLIT, CFK_PS64_WAVES, true>(a, s, reduce);
+            if (kp == 64 && presplit) return launch_solve_t<float, 64, Path::MFMA_SPLIT, PS64_WAVES, true>(a, s, reduce);
             if (kp == 64) return launch_solve_t<float, 64, Path::MFMA_SPLIT, 2>(a, s, reduce);
             if (kp == 128 && presplit) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1, true>(a, s, reduce);
             if (kp == 128) return launch_solve_t<float, 128, Path::MFMA_SPLIT, 1>(a, s, reduce);

@@ -443,6 +443,13 @@ class ALSEngine:
                 "chunk": c.value,
                 "dual_rows": sum(d), "dual_rows_by_blocks": list(d)}
 
+    def split_info(self, side) -> dict:
+        """Split-row plan of the side's block (als_block_split_info): rows split into interleaved chunks, their chunk
+        tasks, the chunk length (entries), whether the half gathers the pre-split table."""
+        v = (ctypes.c_int64 * 4)()
+        call("als_block_split_info", self._h, _side(side), v)
+        return {"interleaved_rows": v[0], "chunk_tasks": v[1], "chunk": v[2], "presplit": bool(v[3])}
+
     def block_stats(self, side):
         a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         call("als_block_stats", self._h, _side(side), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))

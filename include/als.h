@@ -193,6 +193,10 @@ int als_debug_copy_partials(als_engine* e, void* host_dst, int64_t max_bytes, in
 int als_block_path(const als_engine* e, int side, int* gram_path, int* presplit, int64_t* chunk, int64_t* n_dual_rows);
 /* Work-plan statistics of the uploaded block (tasks, partial slots, padded nnz). */
 int als_block_stats(const als_engine* e, int side, int64_t* n_tasks, int64_t* n_reduce, int64_t* nnz_padded);
+/* Split-row plan of the uploaded block (a launch-shape query with no reference counterpart):
+ * info[0] = rows split into interleaved chunks (0: contiguous chunks, the plan of halves whose opposite table fits the
+ * L2s), [1] their chunk tasks, [2] the chunk length in entries, [3] 1 when the half gathers the pre-split table. */
+int als_block_split_info(const als_engine* e, int side, int64_t info[4]);
 
 #ifdef __cplusplus
 }

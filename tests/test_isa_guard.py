@@ -155,29 +155,6 @@ def test_lds_dma_image_waited_before_transposed_reads(kernels):
     assert not bad, bad[:8]
 
 
-def test_double_buffered_dma_counts_match_the_vmcnt(kernels):
-    """The double-buffered pre-split Gram (gram_presplit DBUF, KP = 128) waits `s_waitcnt vmcnt(18)` before reading a
-    block's image: correct only if every block issues exactly 18 vector-memory instructions (its 16 LDS-DMA plus the
-    column-index and rating loads) between consecutive waits, so that the 18 still outstanding are the NEXT block's.
-    Checked on the code object: between two vmcnt(18) waits inside the loop, 18 VMEM ops, 16 of them LDS-DMA."""
-    found = 0
-    for name, ins in _solve_kernels(kernels).items():
-        waits = [i for i, (op, ops) in enumerate(ins) if op == "s_waitcnt" and "vmcnt(18)" in " ".join(ops)]
-        if len(waits) < 2 or not any(op == "global_load_lds_dwordx4" for op, _ in ins):
-            continue   # (compiler-placed vmcnt(18) waits elsewhere are not this scheme)
-        found += 1
-        for a in waits:   # from each wait to the next branch (the loop's break test / back edge) or wait
-            seg = []
-            for op, _ in ins[a + 1:]:
-                if op.startswith("s_cbranch") or op == "s_endpgm":
-                    break
-                seg.append(op)
-            vmem = [op for op in seg if op.startswith(("global_load", "buffer_load", "global_atomic"))]
-            assert len(vmem) == 18 and sum(op == "global_load_lds_dwordx4" for op in vmem) == 16, (name, a, len(vmem))
-    if not found:
-        pytest.skip("no double-buffered pre-split kernel in this build (CFK_PS128_DBUF=0)")
-
-
 def test_fused_dpp_sweep_groups_carry_their_wait_states(kernels):
     """The sweep's fused row-broadcast FMAs (v_fmac_f32_dpp, inline asm in fmac_rowbcast4): a DPP read of a VGPR
     needs 2 wait states after a VALU write of it, and the compiler's hazard recognizer does not see the writes inside

@@ -115,39 +115,12 @@ def main():
                        "finite": bool(torch.isfinite(t).all())}
         diffs[v] = d
         print("vs", args.variants[0], ":", v, json.dumps(d), flush=True)
-    # debug build: cycle accounting of the pipelined launch (one user half per variant)
-    import ctypes
-    from cfk_amd import _lib
-    fn = getattr(_lib.lib(), "als_debug_pc_stats", None)
-    pcstats = {}
-    if fn is not None:
-        names = ["gram", "gram_wait", "solve", "solve_idle", "solves", "tasks", "t_setup", "t_scale", "t_factor",
-                 "t_subst", "t_end"]
-        for v, (e, M, U) in zip(args.variants, engines):
-            buf = (ctypes.c_ulonglong * 16)()
-            if fn(e._h, buf, 1) != 0:
-                continue
-            M.copy_(Ms)
-            U.copy_(Us)
-            e.solve_half(1, 0.05)
-            torch.cuda.synchronize()
-            if fn(e._h, buf, 1) != 0:
-                continue
-            d = dict(zip(names, list(buf)[:len(names)]))
-            if d["solves"]:
-                d["cycles_per_solve"] = d["solve"] / d["solves"]
-                for n in names[6:]:
-                    d[n + "_per_solve"] = d[n] / d["solves"]
-            if d["tasks"]:
-                d["gram_cycles_per_task"] = d["gram"] / d["tasks"]
-            pcstats[v] = d
-            print("pc_stats", v, json.dumps(d), flush=True)
     out = {}
     for v in args.variants:
         out[v] = {k: {"median_ms": statistics.median(x), "min_ms": min(x)} for k, x in res[v].items()}
         out[v]["total_median_ms"] = sum(out[v][k]["median_ms"] for k in ("movie", "user", "movie_reduce", "user_reduce"))
         print(v, json.dumps(out[v]), flush=True)
-    print(json.dumps({"kbench": out, "nnz": args.nnz, "k": args.k, "diffs": diffs, "pc_stats": pcstats}))
+    print(json.dumps({"kbench": out, "nnz": args.nnz, "k": args.k, "diffs": diffs}))
 
 
 if __name__ == "__main__":
