@@ -410,8 +410,9 @@ int check_block_shape(als_engine* e, int64_t n_rows, int64_t row_offset, int64_t
 // Padded entries of a row of degree d (every row starts on a 32-entry block).
 inline int64_t padded(int64_t d) { return (d + cfk::BLOCK_ENTRIES - 1) / cfk::BLOCK_ENTRIES * cfk::BLOCK_ENTRIES; }
 
-// Interleaved split rows: on a half whose opposite table outgrows the L2s (> 32 MB: the 123 MB
-// user table of the Netflix-shape movie half), a row longer than the returned length (entries) is split into
+// Interleaved split rows: on a half whose opposite table outgrows the L2s but fits the Infinity
+// Cache (the 123 / 246 MB user table of the Netflix-shape movie half at k = 64 / 128, the 256 MB item table of the
+// power-law user half), a row longer than the returned length (entries) is split into
 // nc = ceil(d / length) chunks of INTERLEAVED blocks -- chunk c = blocks c, c + nc, c + 2 nc, ... of the row -- so
 // that every chunk covers the row's whole range of opposite slots. With the chunks dispatched together (longest
 // first) the waves of an XCD then walk the opposite table in step and find its rows in their L2. Such a half gathers
@@ -420,7 +421,10 @@ int64_t interleave_chunk(const als_engine* e, int64_t n_opp_rows) {
     const int64_t sb = (n_opp_rows + 1) * (int64_t)cfk::presplit_row_bytes(e->kp);
     if (e->interleave == 0 || e->path != Path::MFMA_SPLIT || (e->kp != 64 && e->kp != 128)) return 0;
     if (n_opp_rows + 1 >= (1 << 24) || sb > (int64_t)UINT32_MAX) return 0;   // the pre-split gather's offsets
-    if (e->interleave < 0 && sb <= (32ll << 20)) return 0;
+    // auto: a table the L2s cannot hold (> 32 MB) that the 256 MiB Infinity Cache still holds; beyond the IC (configs[4]'s
+    // 2.56 GB user table) the contiguous chunks read the long rows' near-dense user ranges in order and win (item half
+    // of the power-law shard: 8.87 vs 14.6 ms interleaved, profiles/r06a)
+    if (e->interleave < 0 && (sb <= (32ll << 20) || sb > (256ll << 20))) return 0;
     // chunk length (kbench, Netflix shape, movie half + its REDUCE, profiles/r06a): k = 64 8,192 / 10,240 / 12,288 /
     // 16,384 / 24,576 entries: 2.07 / 2.04 / 2.06 / 2.16 / 2.29 ms (contiguous chunks: 2.98); k = 128 4,096 / 8,192 /
     // 16,384: 5.76 / 5.32 / 5.06 ms (contiguous: 6.67)
@@ -448,7 +452,8 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     // Interleaved split rows: the long rows' blocks are permuted chunk-major (chunk c = blocks c, c + nc, ... of the
     // row, in order), each chunk one PARTIAL task of whole blocks (the row's last, padded block is the last block of
     // its chunk, so nent counts exactly the chunk's real entries), one REDUCE per row.
-    const int64_t ilv = interleave_chunk(e, n_opp_rows);
+    // (no longer than the contiguous chunk: a small block keeps enough tasks for load balance)
+    const int64_t ilv = std::min(interleave_chunk(e, n_opp_rows), chunk);
     std::vector<int32_t> perm;
     int64_t ilv_rows = 0;
     if (ilv > 0) {
