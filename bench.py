@@ -265,7 +265,10 @@ def main():
         if args.rehearse_one_gpu:
             dist.init_process_group("gloo")
         else:
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+            import datetime
+            # torch's NCCL watchdog bounds its own collectives (the engine bounds the native exchange's waits)
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"),
+                                    timeout=datetime.timedelta(seconds=300))
 
     def barrier():
         if world > 1:
@@ -315,6 +318,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         app.iteration()
+    app.engine.synchronize()   # bounded while an RCCL exchange is pending (als_comm_set_timeout): a hang is named
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -323,6 +327,15 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.rehearse_one_gpu else f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # self-check of a sharded run: every rank's factor replicas bitwise equal, every integrity record clean
+    # (CFK_BENCH_PERTURB_RANK=r: fault injection for tests/test_distributed.py -- rank r alters one word of its
+    # user-factor replica before the check)
+    pr = os.environ.get("CFK_BENCH_PERTURB_RANK")
+    if pr is not None and world > 1 and int(pr) == rank:
+        app.engine.synchronize()
+        app.engine.factors[1][0, 0] += 1.0
+    check = app.verify_replicas()
 
     # per-half device time over the timed steps (HIP events on the launch stream), per half-iteration: with the
     # chunked user half (N > 1) one half is several launches, summed here
@@ -474,6 +487,8 @@ def main():
             "solves_per_s": ((info["movie"]["n_rows"] + info["user"]["n_rows"]) if solo else (nm + nu)) * K / elapsed,
             "projected_job_ratings_per_s_compute_only": value * args.shard_of if solo else None,
             "mse_after": mse,
+            "replicas_agree": check["replicas_agree"], "integrity_clean": check["integrity_clean"],
+            "replica_digest": check["digest"],
             "setup_s": t_setup,
             "build": build,
             "roofline": roofline,
@@ -482,6 +497,11 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if not (check["replicas_agree"] and check["integrity_clean"]):
+        print(f"bench: rank {rank}: self-check failed: replicas_agree={check['replicas_agree']} "
+              f"integrity_clean={check['integrity_clean']} ({check['integrity_failures']} bad partial slots)",
+              file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

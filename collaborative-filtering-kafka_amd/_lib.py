@@ -82,6 +82,7 @@ SIGNATURES = [
     ("als_comm_group_start", _i, []),
     ("als_comm_group_end", _i, []),
     ("als_comm_wait", _i, [_vp]),
+    ("als_comm_set_timeout", _i, [_vp, _i64]),
     ("als_predict", _i, [_vp, _pi64, _i64, _pi64, _i64, _pf]),
     ("als_sq_error", _i, [_vp, _i, _pd, _pi64]),
     ("als_synchronize", _i, [_vp]),

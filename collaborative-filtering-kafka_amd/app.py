@@ -24,6 +24,14 @@ import torch
 from .engine import ALSEngine, Dataset, SIDE_MOVIE, SIDE_USER
 
 
+def _table_digest(t: torch.Tensor) -> int:
+    """Bitwise digest of a factor table (all rows incl. the sentinel): sum over its 32-bit words w_i of
+    w_i * (2 i + 1) * 0x9E3779B1 in wrapping int64 -- any change of one word changes it."""
+    w = t.detach().contiguous().view(torch.int32).flatten().to(torch.int64)
+    i = torch.arange(w.numel(), dtype=torch.int64, device=w.device)
+    return int((w * ((2 * i + 1) * 0x9E3779B1)).sum().item())
+
+
 class ALSApp:
     MOVIE_CHUNK_BYTES = 8 << 20   # a movie factor table above this is exchanged in chunks (N > 1)
 
@@ -197,6 +205,29 @@ class ALSApp:
         return time.perf_counter() - t0
 
     # -------------------------------------------------------------------------------------------------
+    def verify_replicas(self) -> dict:
+        """Self-check of a sharded run (N > 1), after the exchange has settled: every rank's full replicas of both
+        factor matrices must be bitwise identical (what the all-gathers promise: the reference's feature topics
+        deliver the same rows to every partition, ALSApp.java:105-148), and every rank's partial-slot integrity
+        record clean. One digest per side and rank -- a position-weighted int64 sum of the tables' 32-bit words --
+        compared by MIN/MAX all-reduces. Returns {"replicas_agree", "integrity_clean", "digest": [movie, user],
+        "integrity_failures"}; at N = 1 trivially true (one replica)."""
+        self.engine.synchronize()
+        digests = [_table_digest(self.engine.factors[s]) for s in (SIDE_MOVIE, SIDE_USER)]
+        bad = int(self.engine.integrity_status()[0]) if hasattr(self.engine, "integrity_status") else 0
+        if self.world == 1 or self.exchange == "none":
+            return {"replicas_agree": True, "integrity_clean": bad == 0, "digest": [f"{d:016x}" for d in digests],
+                    "integrity_failures": bad}
+        import torch.distributed as dist
+        dev = "cpu" if dist.get_backend(self.group) == "gloo" else self.engine.factors[0].device
+        t = torch.tensor(digests + [bad], dtype=torch.int64, device=dev)
+        hi, lo = t.clone(), t.clone()
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
+        agree = bool(torch.equal(hi[:2], lo[:2]))
+        return {"replicas_agree": agree, "integrity_clean": int(hi[2]) == 0,
+                "digest": [f"{d & 0xFFFFFFFFFFFFFFFF:016x}" for d in digests], "integrity_failures": int(hi[2])}
+
     def factors(self):
         """(U, M) in ascending raw-id order (FeatureCollector.constructFeatureMatrices, :72-88)."""
         U = self.engine.read_factors(SIDE_USER)

@@ -5,11 +5,13 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "als.h"
@@ -132,6 +134,9 @@ struct als_engine {
     hipEvent_t solved = nullptr;         // recorded on `stream` before each all-gather
     hipEvent_t gathered[2] = {nullptr, nullptr};   // last all-gather of each side, on comm_stream
     bool gather_pending[2] = {false, false};
+    int64_t comm_timeout_ms = 120000;    // bound of host waits while a communicator exists (als_comm_set_timeout)
+    int last_gather_side = -1;           // the last all-gather issued (for the timeout's message)
+    int64_t last_gather_chunk = -1, last_gather_rows = 0;
     // Entry-space (als_solve_dual) launches run on side_stream, forked from and joined back into `stream`, so
     // they fill the CUs the main launch's tail leaves idle (ALS_DUAL_SIDE=0: same stream, after the main launch)
     bool dual_side = true;
@@ -164,9 +169,39 @@ int wait_gathers(als_engine* e, bool movie, bool user) {
     return ALS_OK;
 }
 
+// Host wait for the engine's stream, bounded while the engine has a communicator: on expiry the communicator is
+// aborted (so that its kernels end) and the call fails naming the last all-gather issued.
+int stream_wait(als_engine* e, hipStream_t s) {
+    if (!e->comm || e->comm_timeout_ms <= 0) {
+        HIP_TRY(hipStreamSynchronize(s));
+        return ALS_OK;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spin = 0;; ++spin) {
+        const hipError_t st = hipStreamQuery(s);
+        if (st == hipSuccess) return ALS_OK;
+        if (st != hipErrorNotReady) return fail(ALS_ERR_DEVICE, "stream wait: %s", hipGetErrorString(st));
+        const int64_t ms =
+            std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+        if (ms > e->comm_timeout_ms) {
+            (void)ncclCommAbort(e->comm);
+            e->comm = nullptr;
+            return fail(ALS_ERR_COMM,
+                        "rank %d of %d: the engine's stream did not complete within %lld ms; the last RCCL all-gather "
+                        "issued was side %s chunk %lld (%lld rows per shard); communicator aborted",
+                        e->rank, e->world, (long long)e->comm_timeout_ms,
+                        e->last_gather_side == ALS_SIDE_MOVIE ? "movie" : e->last_gather_side == ALS_SIDE_USER ? "user"
+                                                                                                              : "none",
+                        (long long)e->last_gather_chunk, (long long)e->last_gather_rows);
+        }
+        if (spin < 1000) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
 int sync_checked(als_engine* e) {
     if (int r = wait_gathers(e, true, true)) return r;
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (int r = stream_wait(e, e->stream)) return r;
     uint32_t rec[cfk::INTEGRITY_WORDS];
     HIP_TRY(hipMemcpy(rec, e->d_integrity, sizeof(rec), hipMemcpyDeviceToHost));
     if (rec[0] != 0)
@@ -299,6 +334,7 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
     }
     if (const char* env = getenv("ALS_DUAL_SIDE")) e->dual_side = env[0] != '0';
     if (const char* env = getenv("ALS_INTERLEAVE")) e->interleave = env[0] == '0' ? 0 : 1;
+    if (const char* env = getenv("ALS_COMM_TIMEOUT_S")) e->comm_timeout_ms = (int64_t)(atof(env) * 1000.0);
     hipError_t st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (st != hipSuccess) {
         delete e;
@@ -1188,7 +1224,8 @@ int als_synchronize(als_engine* e) {
 int als_integrity_status(als_engine* e, uint32_t* record, int reset) {
     if (int r = check_engine(e)) return r;
     HIP_TRY(hipSetDevice(e->device));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (int r = wait_gathers(e, true, true)) return r;
+    if (int r = stream_wait(e, e->stream)) return r;
     uint32_t rec[cfk::INTEGRITY_WORDS];
     HIP_TRY(hipMemcpy(rec, e->d_integrity, sizeof(rec), hipMemcpyDeviceToHost));
     if (record) std::memcpy(record, rec, sizeof(rec));
@@ -1365,6 +1402,9 @@ int als_allgather_shard(als_engine* e, int side, int64_t slots_per_chunk, int64_
     // chunk-major slots: chunk c holds the G shards' Sc-row pieces back to back, so its exchange is ONE
     // contiguous in-place all-gather
     char* cbase = (char*)f.ptr + (size_t)chunk * (size_t)(Sc * e->world) * row;
+    e->last_gather_side = side;
+    e->last_gather_chunk = chunk;
+    e->last_gather_rows = Sc;
     NCCL_TRY(ncclAllGather(cbase + (size_t)e->rank * Sc * row, cbase, (size_t)Sc * e->kp, dt, e->comm,
                            e->comm_stream));
     if (g_group_depth > 0) {   // placed on the stream at the outermost group end: record the event there
@@ -1391,6 +1431,12 @@ int als_comm_wait(als_engine* e) {
     if (int r = check_engine(e)) return r;
     HIP_TRY(hipSetDevice(e->device));
     return wait_gathers(e, true, true);
+}
+
+int als_comm_set_timeout(als_engine* e, int64_t timeout_ms) {
+    if (int r = check_engine(e)) return r;
+    e->comm_timeout_ms = timeout_ms;
+    return ALS_OK;
 }
 
 int als_block_path(const als_engine* e, int side, int* gram_path, int* presplit, int64_t* chunk, int64_t* n_dual_rows) {

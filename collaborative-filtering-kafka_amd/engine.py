@@ -395,6 +395,10 @@ class ALSEngine:
     def comm_wait(self):
         call("als_comm_wait", self._h)
 
+    def comm_set_timeout(self, timeout_ms: int):
+        """Bound (ms) on the engine's host waits while it has a communicator (als_comm_set_timeout)."""
+        call("als_comm_set_timeout", self._h, int(timeout_ms))
+
     def predict(self, user_rows, movie_rows) -> np.ndarray:
         """FeatureCollector's U M^T (Java-float dots) for the given factor rows, on the GPU."""
         ur = np.ascontiguousarray(user_rows, np.int64)

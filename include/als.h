@@ -157,6 +157,12 @@ int als_comm_group_end(void);
  * its next solve of the other side, and every synchronising call, after them. Work issued by the caller on
  * the engine's stream that reads the gathered replicas (e.g. torch ops) must call als_comm_wait first. */
 int als_comm_wait(als_engine* e);
+/* Bound on every host wait of an engine with a communicator (default 120 000 ms, or ALS_COMM_TIMEOUT_S): a collective
+ * that never completes (a peer gone, mismatched calls) would hang the caller of a synchronising call. On expiry the
+ * communicator is aborted and the call fails with ALS_ERR_COMM naming the last all-gather issued (side, chunk); the
+ * engine is then unusable for the exchange. timeout_ms <= 0: unbounded. (No reference counterpart: the reference's
+ * lost messages hang silently, README.md:241; SURVEY.md section 5 asks for a timeout on collectives.) */
+int als_comm_set_timeout(als_engine* e, int64_t timeout_ms);
 
 /* FeatureCollector's prediction matrix (FeatureCollector.java:90-101) from the resident factors:
  * host_out[u * n_movies + m] = U[user_rows[u]] . M[movie_rows[m]] as a Java float dot (fp32 products and

@@ -133,3 +133,46 @@ def test_sharded_driver_matches_single_process(cfk, oracle_mod, tiny_path, tmp_p
         np.testing.assert_allclose(res["M"], Mo, rtol=1e-12, atol=1e-12)
         # f64 factors -> sum of squared errors in f64 (the stand-in); oracle MSE uses fp32 predictions
         assert abs(float(res["mse"]) - mse_o) < 1e-6
+
+
+def _check_worker(rank, world, port, path, out_dir, perturb_rank):
+    """ALSApp.verify_replicas (bench.py's self-check of a sharded run) over gloo: after the run, and after rank
+    `perturb_rank` alters one word of its user-factor replica (-1: none)."""
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch.distributed as dist
+    import __graft_entry__
+    cfk = __graft_entry__.load_package()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ds = cfk.Dataset.load_netflix(path)
+    app = cfk.ALSApp(4, 10, 0.05, 2, precision="f64", seed=42, rank=rank, world_size=world, overlap_chunks=2)
+    app.setup(ds, engine_factory=OracleShardEngine)
+    app.run()
+    before = app.verify_replicas()
+    if rank == perturb_rank:
+        app.engine.factors[1][3, 1] += 1e-9
+    after = app.verify_replicas()
+    with open(os.path.join(out_dir, f"check{rank}.json"), "w") as f:
+        json.dump({"before": before, "after": after}, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,perturb", [(2, 1), (3, 0), (3, -1)])
+def test_replica_self_check(tiny_path, tmp_path, world, perturb):
+    """The multi-GPU run's self-check (bench.py fields replicas_agree / integrity_clean): every rank's replicas of both
+    factor matrices agree bitwise after the exchange; one word changed on one rank flips replicas_agree on EVERY rank
+    (bench.py then exits with status 3), the digests of the other ranks unchanged."""
+    import json
+    import torch.multiprocessing as mp
+    mp.spawn(_check_worker, args=(world, _free_port(), tiny_path, str(tmp_path), perturb), nprocs=world, join=True)
+    res = [json.load(open(os.path.join(tmp_path, f"check{r}.json"))) for r in range(world)]
+    for r in res:
+        assert r["before"]["replicas_agree"] and r["before"]["integrity_clean"], r
+        assert r["after"]["replicas_agree"] == (perturb < 0), r
+        assert r["after"]["integrity_clean"]
+    assert len({tuple(r["before"]["digest"]) for r in res}) == 1
+    for i, r in enumerate(res):
+        assert (r["after"]["digest"] == r["before"]["digest"]) == (i != perturb)

@@ -324,5 +324,15 @@ def test_bench_rehearsal_two_ranks_shard_restricted(tmp_path):
     assert l2["config"]["nnz_this_rank"] < 0.75 * 600_000
     assert abs(l2["mse_after"] - l1["mse_after"]) <= 1e-9 * l1["mse_after"]
     assert l1["build"]["lib_sha256"] == l2["build"]["lib_sha256"]
+    # the self-check of a sharded run: replicas bitwise equal on both ranks, integrity clean
+    assert l2["replicas_agree"] is True and l2["integrity_clean"] is True and len(l2["replica_digest"]) == 2
+    # fault injection: rank 1 alters one word of its replica -> replicas_agree false, exit status 3
+    bad = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port + 1), os.path.join(ROOT, "bench.py"),
+                          "--gpus", "2", "--rehearse-one-gpu"] + common, capture_output=True, text=True, timeout=300,
+                         env=dict(env, CFK_BENCH_PERTURB_RANK="1"), cwd=ROOT)
+    assert bad.returncode != 0 and "self-check failed" in bad.stderr, bad.stderr[-2000:]
+    lb = json.loads([x for x in bad.stdout.splitlines() if x.startswith("{")][-1])
+    assert lb["replicas_agree"] is False and lb["integrity_clean"] is True
     if not os.environ.get("CFK_ALS_LIB"):   # the product library (an A/B variant carries no build stamp)
         assert l1["build"]["source_matches_tree"] and l1["build"]["binary_matches_tree"]

@@ -535,6 +535,33 @@ def test_row_layout_scatters_rows_into_chunk_major_slots(cfk, oracle_mod):
     assert cnt == cnt_o and se == pytest.approx(se_o, rel=1e-4)
 
 
+def test_comm_timeout_names_the_pending_exchange(cfk, oracle_mod):
+    """als_comm_set_timeout: with a communicator, the engine's host waits are bounded; a stream still busy past the
+    bound fails the synchronising call with ALS_ERR_COMM naming the last all-gather issued (side, chunk), the
+    communicator aborted -- the diagnosis a hung exchange gets instead of a hang. Forced here with a 1-ms bound behind
+    a queue of real halves on a one-rank communicator (whose kernels all complete)."""
+    from cfk_amd._lib import ALSError
+    ds = cfk.Dataset.synthetic_netflix(n_users=60_000, n_movies=2_000, nnz=3_000_000, seed=11, nthreads=8)
+    eng = cfk.ALSEngine(64, "f32")
+    eng.comm_init(1, 0, cfk.ALSEngine.comm_unique_id())
+    info = [ds.shard_info(s) for s in (0, 1)]
+    for side in (0, 1):
+        c = ds.shard_coo(side)
+        eng.alloc_factors(side, info[side]["n_slots"])
+        eng.set_block_coo(side, c["n_rows"], c["rows"], c["cols"], c["ratings"], 0, info[1 - side]["n_slots"])
+    eng.write_factors(1, ds.init_user_factors(64, 3))
+    eng.synchronize()
+    eng.comm_set_timeout(1)
+    for _ in range(40):
+        eng.solve_half(0, LAM)
+        eng.allgather_shard(0, info[0]["slots_per_shard"])
+        eng.solve_half(1, LAM)
+        eng.allgather_shard(1, info[1]["slots_per_shard"])
+    with pytest.raises(ALSError, match="ALS_ERR_COMM.*side user chunk 0"):
+        eng.synchronize()
+    eng.close()   # drains the stream: the queued kernels all complete
+
+
 def test_comm_init_group_one_engine(cfk):
     e = cfk.ALSEngine(16, "f32")
     cfk.ALSEngine.comm_init_group([e])
