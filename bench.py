@@ -37,6 +37,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_MEASURED_GBS = 6290.0    # the guide's measured HBM rate (float4 copy, 79 % of the spec)
 FP32_PEAK_TFS = 157.3        # f32 vector = f32 MFMA dense peak
 MFMA16_PEAK_TFS = 2500.0     # dense bf16 / f16 MFMA peak (no sparsity; the f16 forms take the bf16 cycles)
 # MI355X_MICROARCH.md "Indexed rows: gather into LDS": uniformly random rows of a 151 MB table (the 123 MB k = 64
@@ -70,6 +71,25 @@ def mfma_per_block(kp, presplit):
     if presplit:
         return 3 * (c * (c - 1) // 2) + 2 * c + 2 * c
     return 6 * (c * (c - 1) // 2) + 4 * c
+
+
+def served_from(table_bytes, interleaved):
+    """Where a half's gathered opposite rows are served from, and that source's gather ceiling (GB/s): the XCD's L2
+    (a table of <= 8 MB), the Infinity Cache (<= 256 MiB), beyond it a mix of IC and HBM ("hbm": the SURVEY.md §8d
+    roofline binds), or -- a half with interleaved split rows -- the L2 as far as the walk in step keeps the
+    IC-resident table's rows there ("l2_ic_walk", priced against the L2 ceiling: an upper bound)."""
+    if interleaved:
+        return "l2_ic_walk", L2_GATHER_CEILING_GBS
+    if table_bytes <= L2_RESIDENT_BYTES:
+        return "l2", L2_GATHER_CEILING_GBS
+    if table_bytes <= IC_RESIDENT_BYTES:
+        return "ic", IC_GATHER_CEILING_GBS
+    return "hbm", HBM_PEAK_GBS
+
+
+def bound_label(where):
+    """roofline.bound of a gather-limited launch by where its rows are served from"""
+    return "beyond_ic_mixed" if where == "hbm" else f"{where}_gather"
 
 
 def cpu_model():
@@ -228,7 +248,7 @@ def main():
                          "torch.distributed (RCCL); the one-GPU gloo rehearsal always uses torch")
     ap.add_argument("--movie-chunks", type=int, default=None,
                     help="N > 1: movie-half exchange chunks (default: --overlap-chunks once the movie table exceeds "
-                         "8 MB, e.g. configs[4]; else 1)")
+                         "64 MB, e.g. configs[4]; else 1)")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="G > 1: run ONE rank's work of a G-GPU job on this GPU (shard --shard-rank of G, synthesized "
                          "alone, no exchange): the per-GPU compute of a sharded config such as configs[4] on 8 GPUs; "
@@ -377,9 +397,12 @@ def main():
                         + 4 * kp * i["n_rows"])
             opp_rows = info["user" if side == "movie" else "movie"]["n_slots"] + 1
             table_bytes = opp_rows * 4 * kp
-            # where the gathered rows are served from: the XCD's L2, the Infinity Cache, or (beyond it) HBM
-            where = "l2" if table_bytes <= L2_RESIDENT_BYTES else "ic" if table_bytes <= IC_RESIDENT_BYTES else "hbm"
-            gceil = {"l2": L2_GATHER_CEILING_GBS, "ic": IC_GATHER_CEILING_GBS, "hbm": HBM_PEAK_GBS}[where]
+            # where the gathered rows are served from: the XCD's L2, the Infinity Cache, (beyond it) HBM -- or, on a
+            # half with interleaved split rows, the L2 as far as the waves' walk of the
+            # IC-resident table in step keeps its rows there: priced against the L2 gather ceiling (an upper bound;
+            # the rest of the rows come from the IC)
+            split = eng.split_info(si)
+            where, gceil = served_from(table_bytes, split["interleaved_rows"] > 0)
             mfma_frac = mf / t_s / 1e12 / MFMA16_PEAK_TFS if mf else 0.0
             # rows of a table beyond the L2 are served by the Infinity Cache: measure them with the fabric-side counter
             # bytes of this build (L2 hits excluded) when profiled, else with the bytes requested (then an upper
@@ -404,7 +427,10 @@ def main():
                            "opposite_table_bytes": table_bytes, "served_from": where,
                            "achieved_gbs": g_bytes / t_s / 1e9, "ceiling_gbs": gceil, "frac": gather_frac,
                            "ceiling": {"l2": "L2-resident rows", "ic": "Infinity-Cache random rows",
-                                       "hbm": "HBM peak (table beyond the Infinity Cache)"}[where]},
+                                       "hbm": "HBM peak (table beyond the Infinity Cache)",
+                                       "l2_ic_walk": "L2-resident rows (an IC-resident table walked in step by "
+                                                     "interleaved chunks)"}[where]},
+                "split_rows": split,
                 "algorithmic_bytes": {"bytes": b, "achieved_gbs": b / t_s / 1e9, "frac_of_hbm": b / t_s / 1e9 / HBM_PEAK_GBS,
                                       "note": "SURVEY.md §8d algorithmic bytes / launch time; cache-served gathers "
                                               "included, so it can exceed 1: not a bound"},
@@ -423,11 +449,17 @@ def main():
                          limit="MFMA pipe: the Gram's 16x16x32 MFMA flops as issued (whole launch, solve phase "
                                "included) against the dense bf16/f16 peak")
             elif where == "hbm":
-                d.update(bound="hbm", unit="GB/s", peak=gceil, achieved=g_bytes / t_s / 1e9, frac=gather_frac,
-                         limit="HBM: SURVEY.md §8d algorithmic bytes per launch / launch time against the 8 TB/s HBM "
-                               "peak (the gathered table exceeds the 256 MiB Infinity Cache)")
+                # the table exceeds the IC, but its hot rows (the most active users) stay there: a mix of IC and
+                # HBM service, so the algorithmic rate is reported against the spec peak AND the measured HBM rate
+                d.update(bound=bound_label(where), unit="GB/s", peak=gceil, achieved=g_bytes / t_s / 1e9,
+                         frac=gather_frac, frac_of_measured_hbm=g_bytes / t_s / 1e9 / HBM_MEASURED_GBS,
+                         measured_hbm_gbs=HBM_MEASURED_GBS,
+                         limit="SURVEY.md §8d algorithmic bytes per launch / launch time against the 8 TB/s HBM peak "
+                               "(frac) and the guide's measured 6.29 TB/s (frac_of_measured_hbm); the gathered table "
+                               "exceeds the 256 MiB Infinity Cache but its most active rows are served from it, so "
+                               "this is a mixed IC/HBM figure, not a pure HBM bound")
             else:
-                d.update(bound=f"{where}_gather", unit="GB/s", peak=gceil, achieved=g_bytes / t_s / 1e9,
+                d.update(bound=bound_label(where), unit="GB/s", peak=gceil, achieved=g_bytes / t_s / 1e9,
                          frac=gather_frac,
                          limit="gather of the opposite factor rows: bytes requested per launch / launch time against "
                                f"the chip's {d['gather']['ceiling']} gather ceiling (MI355X_MICROARCH.md)")
@@ -438,6 +470,7 @@ def main():
             "bound": d["bound"], "limiter": d["bound"],
             "achieved": d["achieved"], "peak": d["peak"],
             "unit": d["unit"], "frac": d["frac"], "traffic": d.get("traffic"),
+            "frac_of_measured_hbm": d.get("frac_of_measured_hbm"),
             "kernel": d["kernel"] + f" ({dom} half, the dominant launch)", "limit": d["limit"],
             "avg_launch_ms": d["avg_launch_ms"], "counters": d.get("counters"),
             "counters_dropped": ctr_why,
@@ -451,8 +484,10 @@ def main():
             "note": "achieved/frac: the dominant launch against the ceiling it is closest to (bound: mfma = "
                     "executed 16x16x32 MFMA flops against the dense bf16/f16 peak; l2_gather / ic_gather = the "
                     "gathered bytes it requests / launch time against the chip's gather ceiling for rows served from "
-                    "the L2 / the Infinity Cache (MI355X_MICROARCH.md); hbm = SURVEY.md §8d algorithmic bytes against "
-                    "the HBM peak when the gathered table exceeds the Infinity Cache); traffic = PMC FETCH_SIZE x2 + "
+                    "the L2 / the Infinity Cache (MI355X_MICROARCH.md); l2_ic_walk_gather = an IC-resident table "
+                    "walked in step by interleaved split rows, priced against the L2 ceiling; beyond_ic_mixed = "
+                    "SURVEY.md §8d algorithmic bytes against the HBM peak and the measured HBM rate when the gathered "
+                    "table exceeds the Infinity Cache); traffic = PMC FETCH_SIZE x2 + "
                     "WRITE_SIZE per launch; counters = rocprofv3 SQ passes of this build",
         }
         cpu = None

@@ -33,7 +33,11 @@ def _table_digest(t: torch.Tensor) -> int:
 
 
 class ALSApp:
-    MOVIE_CHUNK_BYTES = 8 << 20   # a movie factor table above this is exchanged in chunks (N > 1)
+    # a movie factor table above this is exchanged in chunks (N > 1): configs[4]'s 256 MB item table (all-gather ~1.7 ms
+    # at G = 8), not the 9 MB k = 128 Netflix one -- its 4 chunk launches cost more in launch tails than the overlap of a
+    # ~0.1 ms all-gather saves (one rank's k = 128 movie half at G = 2: 7.2 ms in 4 launches vs 5.4 ms in one,
+    # profiles/r06a)
+    MOVIE_CHUNK_BYTES = 64 << 20
 
     def __init__(self, num_partitions: int, num_features: int, als_lambda: float, num_als_iterations: int,
                  num_movies: int | None = None, num_users: int | None = None, *, precision: str = "f32",

@@ -453,7 +453,7 @@ inline int64_t padded(int64_t d) { return (d + cfk::BLOCK_ENTRIES - 1) / cfk::BL
 // that every chunk covers the row's whole range of opposite slots. With the chunks dispatched together (longest
 // first) the waves of an XCD then walk the opposite table in step and find its rows in their L2. Such a half gathers
 // the pre-split table (the fp16 Gram). 0: contiguous chunks at chunk_entries() (the other halves).
-int64_t interleave_chunk(const als_engine* e, int64_t n_opp_rows) {
+int64_t interleave_chunk(const als_engine* e, int64_t n_opp_rows, const std::vector<int64_t>& deg) {
     const int64_t sb = (n_opp_rows + 1) * (int64_t)cfk::presplit_row_bytes(e->kp);
     if (e->interleave == 0 || e->path != Path::MFMA_SPLIT || (e->kp != 64 && e->kp != 128)) return 0;
     if (n_opp_rows + 1 >= (1 << 24) || sb > (int64_t)UINT32_MAX) return 0;   // the pre-split gather's offsets
@@ -461,10 +461,26 @@ int64_t interleave_chunk(const als_engine* e, int64_t n_opp_rows) {
     // 2.56 GB user table) the contiguous chunks read the long rows' near-dense user ranges in order and win (item half
     // of the power-law shard: 8.87 vs 14.6 ms interleaved, profiles/r06a)
     if (e->interleave < 0 && (sb <= (32ll << 20) || sb > (256ll << 20))) return 0;
-    // chunk length (kbench, Netflix shape, movie half + its REDUCE, profiles/r06a): k = 64 8,192 / 10,240 / 12,288 /
-    // 16,384 / 24,576 entries: 2.07 / 2.04 / 2.06 / 2.16 / 2.29 ms (contiguous chunks: 2.98); k = 128 4,096 / 8,192 /
-    // 16,384: 5.76 / 5.32 / 5.06 ms (contiguous: 6.67)
-    int64_t len = e->kp == 128 ? 16384 : 10240;
+    auto long_work = [&](int64_t t) {   // entries in rows longer than t
+        int64_t w = 0;
+        for (int64_t d : deg) w += d > t ? d : 0;
+        return w;
+    };
+    // the walk in step needs many chunks in flight: resident waves of the pre-split launch (4 per SIMD at KP = 64, 1 at
+    // KP = 128). Chunk length (kbench, Netflix shape, movie half + its REDUCE, profiles/r06a): k = 64, whole data:
+    // 8,192 / 10,240 / 12,288 / 16,384 / 24,576 entries 2.07 / 2.04 / 2.06 / 2.16 / 2.29 ms (contiguous chunks: 2.98);
+    // one rank's shard of G = 2 / 4 / 8 (fewer chunks than twice the resident waves): 1.52 / 0.95 / 0.66 ms at the
+    // best length vs 1.58 / 0.90 / 0.47 contiguous -- so k = 64 interleaves only with >= 1.5 x the resident waves of
+    // chunks. k = 128 (whole data 4,096 / 8,192 / 16,384: 5.76 / 5.32 / 5.06 ms, contiguous 6.67; shards of G = 2 / 4
+    // / 8 at 8,192: 4.92 / 2.55 / 1.37 vs 5.25 / 2.77 / 1.50) always, about 4 chunks per resident wave, 8k..16k long.
+    const int64_t conc = (int64_t)std::max(1, e->cu_count) * (e->kp == 128 ? 4 : 16);
+    int64_t len;
+    if (e->kp == 64) {
+        len = 10240;
+        if (e->interleave < 0 && long_work(len) < len * conc * 3 / 2) return 0;
+    } else {
+        len = std::min<int64_t>(16384, std::max<int64_t>(8192, long_work(16384) / (4 * conc)));
+    }
 #ifdef CFK_DEBUG_KNOBS
     if (const char* v = getenv("ALS_ILV_CHUNK")) len = std::max(32L, atol(v));
 #endif
@@ -489,7 +505,7 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     // row, in order), each chunk one PARTIAL task of whole blocks (the row's last, padded block is the last block of
     // its chunk, so nent counts exactly the chunk's real entries), one REDUCE per row.
     // (no longer than the contiguous chunk: a small block keeps enough tasks for load balance)
-    const int64_t ilv = std::min(interleave_chunk(e, n_opp_rows), chunk);
+    const int64_t ilv = std::min(interleave_chunk(e, n_opp_rows, deg), chunk);
     std::vector<int32_t> perm;
     int64_t ilv_rows = 0;
     if (ilv > 0) {

@@ -111,8 +111,10 @@ int als_read_factors(als_engine* e, int side, int64_t row0, int64_t n_rows, void
 
 /* ---- THE HOT PATH ------------------------------------------------------------------------------- */
 /* For every row j of `side`'s block: gather Y_S = opposite factor rows of its in-block, form
- * A = Y_S^T Y_S + lambda * n_j * I and V = Y_S^T r, solve A m_j = V (Cholesky; A is SPD because
- * lambda * n_j > 0) and store m_j. == MFeatureCalculator.java:66-104 / UFeatureCalculator.java:66-104
+ * A = Y_S^T Y_S + lambda * n_j * I and V = Y_S^T r, solve A m_j = V and store m_j. A is SPD because lambda * n_j > 0:
+ * the MFMA paths (fp32 k <= 128, fp64 k <= 64) factor it as a Jacobi-scaled block LDL^T on the 16 x 16 Gram tiles
+ * with a pivot-gated refinement step, the generic path (wider k) by Cholesky; EJML's LU inverse (the reference,
+ * CommonOps_FDRM.invert) is restated in the oracle. == MFeatureCalculator.java:66-104 / UFeatureCalculator.java:66-104
  * for the whole partition. Asynchronous on the engine's stream. */
 int als_solve_half(als_engine* e, int side, float lambda);
 
@@ -192,8 +194,10 @@ int als_timing_collect(als_engine* e, int side, double* ms_gram, double* ms_redu
  * last half) to host memory and reports its size. Synchronising. */
 int als_debug_copy_partials(als_engine* e, void* host_dst, int64_t max_bytes, int64_t* bytes);
 /* Gram variant of `side`'s block: gram_path 0 = LDS-staged VALU (fp64, fp32 k < 32), 1 = fp32 MFMA
- * (v_mfma_f32_16x16x4_f32), 2 = split-bf16 MFMA; presplit = 1 when the opposite table is gathered as pre-split
- * bf16 pieces (RHS on the MFMAs too); chunk = entries per PARTIAL task of a split row; n_dual_rows[3] = short rows
+ * (v_mfma_f32_16x16x4_f32), 2 = split MFMA (fp32 operands split exactly into narrow terms); presplit = 1 when the
+ * opposite table is gathered as the pre-split scaled two-term fp16 copy (h + m per value, RHS on the MFMAs too),
+ * 0 when each gathered fp32 row is split on the fly into three bf16 terms; chunk = entries per contiguous PARTIAL
+ * task of a split row (interleaved split rows: als_block_split_info); n_dual_rows[3] = short rows
  * of 1, 2 and 3 padded blocks solved in entry space, (Y Y^T + lambda n I) alpha = r, m = Y^T alpha (the same
  * solution as the k x k system). */
 int als_block_path(const als_engine* e, int side, int* gram_path, int* presplit, int64_t* chunk, int64_t* n_dual_rows);

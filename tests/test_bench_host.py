@@ -143,3 +143,17 @@ def test_prof_summary_sums_the_chunk_launches_of_each_half(tmp_path, monkeypatch
     assert c["per_side"]["movie"]["hbm_bytes"] == 2 * (10 * 1024 * 2 + 1024)
     assert c["per_side"]["user"]["hbm_bytes"] == 3 * (10 * 1024 * 2 + 1024)
     assert c["lib_sha256"] == "a" * 64 and c["device_code_sha256"] == "d" * 64
+
+
+def test_roofline_source_labels():
+    """Where a half's gathered rows come from and the label its roofline line carries: the
+    configs[4] user table (2.56 GB, beyond the 256 MiB Infinity Cache) is a mixed IC/HBM figure, not a pure HBM
+    bound; an interleaved half walks its IC-resident table in step (priced against the L2 ceiling)."""
+    assert bench.served_from(17_771 * 256, False) == ("l2", bench.L2_GATHER_CEILING_GBS)
+    assert bench.served_from(480_190 * 256, False) == ("ic", bench.IC_GATHER_CEILING_GBS)
+    assert bench.served_from(10_000_001 * 256, False) == ("hbm", bench.HBM_PEAK_GBS)
+    assert bench.served_from(480_190 * 256, True) == ("l2_ic_walk", bench.L2_GATHER_CEILING_GBS)
+    assert bench.bound_label("hbm") == "beyond_ic_mixed"
+    assert bench.bound_label("l2_ic_walk") == "l2_ic_walk_gather"
+    assert bench.bound_label("ic") == "ic_gather"
+    assert bench.HBM_MEASURED_GBS < bench.HBM_PEAK_GBS

@@ -30,13 +30,18 @@ def main():
     ap.add_argument("--users", type=int, default=480_189)
     ap.add_argument("--movies", type=int, default=17_770)
     ap.add_argument("--nnz", type=int, default=100_000_000)
+    ap.add_argument("--shard-of", type=int, default=1, help="G > 1: shard 0 of G (one rank's blocks, bench --shard-of)")
     args = ap.parse_args()
     import numpy as np
     import torch
     import __graft_entry__
     cfk = __graft_entry__.load_package()
-    ds = cfk.Dataset.synthetic_netflix(args.users, args.movies, args.nnz, 0xA15, nthreads=16)
-    blocks = [ds.shard_block(0), ds.shard_block(1)]
+    G = args.shard_of
+    if G > 1:
+        ds = cfk.Dataset.synthetic_shard("netflix", args.users, args.movies, args.nnz, 0xA15, G, 0, nthreads=16)
+    else:
+        ds = cfk.Dataset.synthetic_netflix(args.users, args.movies, args.nnz, 0xA15, nthreads=16)
+    blocks = [ds.shard_block(0, G, 0), ds.shard_block(1, G, 0)]
     kp = cfk.factor_stride(args.k)
 
     def tables():
@@ -55,7 +60,7 @@ def main():
         eng.bind_factors(1, U)
         for side in (0, 1):
             b = blocks[side]
-            eng.set_block(side, b["row_ptr"], b["col"], b["ratings"], 0, blocks[1 - side]["n_slots"])
+            eng.set_block(side, b["row_ptr"], b["col"], b["ratings"], b["row_offset"], blocks[1 - side]["n_slots"])
         os.environ.clear()
         os.environ.update(saved)
         return eng
@@ -66,7 +71,7 @@ def main():
     # so the clock, depends on the operand values).
     Ms, Us = tables()
     ref = make_engine("", Ms, Us)
-    ref.write_factors(1, ds.init_user_factors(args.k, 42))
+    ref.write_factors(1, ds.init_user_factors(args.k, 42, G))
     for _ in range(2):
         ref.solve_half(0, 0.05)
         ref.solve_half(1, 0.05)
