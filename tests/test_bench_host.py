@@ -106,8 +106,8 @@ def test_prof_summary_sums_the_chunk_launches_of_each_half(tmp_path, monkeypatch
     import prof_summary
     monkeypatch.setattr(prof_summary, "ROOT", str(tmp_path))
     src = tmp_path / "gpurun_out" / "prof_t"
-    main_k = "void cfk::(anonymous namespace)::als_solve_mfma<64, 2, true, false, false, false, 0, false, false>(x)"
-    red_k = "void cfk::(anonymous namespace)::als_solve_mfma<64, 2, false, false, true, false, 0, false, false>(x)"
+    main_k = "void cfk::(anonymous namespace)::als_solve_mfma<64, 2, true, false, false, false>(x)"
+    red_k = "void cfk::(anonymous namespace)::als_solve_mfma<64, 2, false, false, true, false>(x)"
     rows, pmc, did, t = [], [], 0, 0
     for it in range(3):
         for half, n in (("movie", 2), ("user", 3)):

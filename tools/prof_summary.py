@@ -30,8 +30,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def mfma_args(name):
-    """template arguments of an als_solve_mfma instantiation: <KP, MINW, SPLIT, PRESPLIT, REDUCE, NOE, RHS, GRIDLOOP,
-    DBUF> (als_kernels.hip)"""
+    """template arguments of an als_solve_mfma instantiation: <KP, MINW, SPLIT, PRESPLIT, REDUCE, GRIDLOOP>
+    (als_kernels.hip)"""
     if "als_solve_mfma<" not in name:
         return None
     return [a.strip() for a in name.split("als_solve_mfma<", 1)[1].split(">")[0].split(",")]
@@ -45,7 +45,7 @@ def is_reduce(name):
 def is_fallback(name):
     """the pre-split range guard's grid-stride fallback launch (waves exit at once while the table is in range)"""
     a = mfma_args(name)
-    return bool(a) and len(a) > 7 and a[7] == "true"
+    return bool(a) and len(a) > 5 and a[5] == "true"
 
 
 def role_of(name, grid, grids):
@@ -169,7 +169,7 @@ def main(tag, name, launches=None):
                              "write_bytes": write[role]["WRITE_SIZE"] * 1024}
             traffic[role]["hbm_bytes"] = traffic[role]["fetch_bytes_x2"] + traffic[role]["write_bytes"]
     out["traffic"] = traffic
-    for pas in ("sq", "sq_gram", "lds"):
+    for pas in ("sq", "sq_gram", "lds", "l2"):
         sq = per_role(f"{src}/{pas}/**/*counter_collection.csv")
         res = {}
         for role, c in sq.items():
@@ -183,6 +183,8 @@ def main(tag, name, launches=None):
             if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "GRBM_GUI_ACTIVE" in c:
                 # MFMA busy cycles are summed over all SIMDs (1024); GRBM_GUI_ACTIVE over the 8 XCDs
                 d["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8 * 1024)
+            if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c and c["TCC_HIT_sum"] + c["TCC_MISS_sum"] > 0:
+                d["l2_hit_frac"] = c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
             if "SQ_WAIT_INST_ANY" in c and "SQ_WAVE_CYCLES" in c:
                 d["wait_inst_any_frac"] = c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"]
                 d["wait_any_frac"] = c.get("SQ_WAIT_ANY", 0) / c["SQ_WAVE_CYCLES"]
@@ -226,6 +228,9 @@ def main(tag, name, launches=None):
                         "mfma_busy_frac": (sq["SQ_VALU_MFMA_BUSY_CYCLES"] - gr["SQ_VALU_MFMA_BUSY_CYCLES"]) / (scyc * SIMDS),
                         "valu_issue_frac": (sq["SQ_INSTS_VALU"] - gr["SQ_INSTS_VALU"]) / (scyc * SIMDS),
                         "note": "whole launch minus the Gram-only launch of the same blocks (debug build)"}
+        l2 = out.get("l2", {}).get(side)
+        if l2 and "l2_hit_frac" in l2:
+            d["l2_hit_frac"] = l2["l2_hit_frac"]
         ld = out.get("lds", {}).get(side)
         if ld:
             d["lds"] = {x: ld[x] for x in ("lds_bank_conflict_frac", "lds_active_frac", "wait_inst_lds_frac") if x in ld}

@@ -4,6 +4,7 @@
 #   trace/                rocprofv3 --kernel-trace --stats of a 20-step bench run (kernel_stats.csv)
 #   fetch/, write/        one PMC pass each: FETCH_SIZE, WRITE_SIZE (they cannot share a pass)
 #   lds/                  LDS counters (bank-conflict and LDS-array cycles, LDS issue stalls) of the full launches
+#   l2/                   L2 hits and misses (TCC_HIT_sum, TCC_MISS_sum): the share of the gathers the L2 serves
 #   sq/, sq_gram/         SQ counters of the full launches, and of the Gram alone (ALS_DEBUG_SKIP_SOLVE=1, which only
 #                         the debug build honours: collaborative-filtering-kafka_amd/build_debug, `make debug`)
 # Every GPU step has its own time limit; a fault, abort or timeout ends the script (no further GPU step).
@@ -38,4 +39,5 @@ CFK_ALS_LIB=$R/collaborative-filtering-kafka_amd/build_debug/libcfk_als.so \
     --rounds 2 --variants ALS_DEBUG_SKIP_SOLVE=1 $KB
 LDS="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_VALU_MFMA_COEXEC_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
 step 300 lds.log rocprofv3 --pmc $LDS -d "$O/lds" -o run --output-format csv -- python3 "$R/bench.py" $P
+step 300 l2.log rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$O/l2" -o run --output-format csv -- python3 "$R/bench.py" $P
 echo "profile_round $tag done"
