@@ -472,14 +472,17 @@ int64_t interleave_chunk(const als_engine* e, int64_t n_opp_rows, const std::vec
     // one rank's shard of G = 2 / 4 / 8 (fewer chunks than twice the resident waves): 1.52 / 0.95 / 0.66 ms at the
     // best length vs 1.58 / 0.90 / 0.47 contiguous -- so k = 64 interleaves only with >= 1.5 x the resident waves of
     // chunks. k = 128 (whole data 4,096 / 8,192 / 16,384: 5.76 / 5.32 / 5.06 ms, contiguous 6.67; shards of G = 2 / 4
-    // / 8 at 8,192: 4.92 / 2.55 / 1.37 vs 5.25 / 2.77 / 1.50) always, about 4 chunks per resident wave, 8k..16k long.
+    // / 8 at 8,192: 4.92 / 2.55 / 1.37 vs 5.25 / 2.77 / 1.50) always. Round 6 (profiles/r06c/xcd2_*.log, movie half +
+    // REDUCE): whole data 16,384 / 8,192 / 4,096: 5.07 / 5.26 / 5.71 ms; shards of G = 2 / 4 / 8 at 4,096: 4.17 / 2.36 /
+    // ~1.40 ms vs 4.98 / 2.57 / 1.39 at 8,192 (2,048: 4.13 / 2.29 / 1.40; its REDUCE launch doubles) -- so 16,384 when
+    // the long rows hold over ~4 chunks of it per resident wave (the whole Netflix shape), else 4,096.
     const int64_t conc = (int64_t)std::max(1, e->cu_count) * (e->kp == 128 ? 4 : 16);
     int64_t len;
     if (e->kp == 64) {
         len = 10240;
         if (e->interleave < 0 && long_work(len) < len * conc * 3 / 2) return 0;
     } else {
-        len = std::min<int64_t>(16384, std::max<int64_t>(8192, long_work(16384) / (4 * conc)));
+        len = long_work(16384) >= 16384 * 4 * conc ? 16384 : 4096;
     }
 #ifdef CFK_DEBUG_KNOBS
     if (const char* v = getenv("ALS_ILV_CHUNK")) len = std::max(32L, atol(v));

@@ -558,16 +558,29 @@ __device__ __forceinline__ void fmac_rowbcast4(f32x4& a, float t) {
     a[2] = a2;
     a[3] = a3;
 }
+// lane L ? x : v with the lane mask a scalar constant (s_mov): the compiler's select re-derived the mask by a
+// v_cmp at every pivot step (one vector instruction, and a 2-state hazard before the v_cndmask reading it).
+// AFTER_DPP: ends with the 2 wait states a following DPP read of the result needs (see fmac_rowbcast4).
+template <int L, bool AFTER_DPP>
+__device__ __forceinline__ float select_lane(float v, float x) {
+    float r;
+    if constexpr (AFTER_DPP)
+        asm("v_cndmask_b32_e64 %0, %1, %2, %3\n\ts_nop 1" : "=v"(r) : "v"(v), "v"(x), "s"((uint64_t)1 << L));
+    else
+        asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(v), "v"(x), "s"((uint64_t)1 << L));
+    return r;
+}
 template <int p>
 __device__ __forceinline__ void sweep_step(f32x4& a, int lane, float& nrd_min) {
     constexpr int pg = p >> 2, pr = p & 3;
     const float nrd = __builtin_amdgcn_rcpf(-bcast(a[pr], 16 * pg + p));   // -1 / d
     nrd_min = fminf(nrd_min, nrd);                                          // -1 / (smallest pivot)
-    const bool piv = lane == 16 * pg + p;   // 16 lane masks, CSE-d across the 4 diagonal tiles (SGPRs)
-    a[pr] = piv ? a[pr] - 1.f : a[pr];
+    // the pivot lane's d - 1 (read next by v_readlane / ds_bpermute / the DPP block, which waits its own 2 states)
+    a[pr] = select_lane<16 * pg + p, false>(a[pr], a[pr] - 1.f);
     const float t = col_bcast<pg>(a[pr]) * nrd;   // a[p][c] (d - 1 at c = p) * (-1/d)
     fmac_rowbcast4<p>(a, t);                       // a[4g + r][c] += a[4g + r][p] t[c]
-    a[pr] = piv ? nrd : a[pr];
+    a[pr] = select_lane<16 * pg + p, true>(a[pr], nrd);
+    (void)lane;
 }
 __device__ __forceinline__ void sweep_tile(f32x4& a, int lane, float& nrd_min) {
     static_for<0, 16>([&](auto P_) { sweep_step<decltype(P_)::value>(a, lane, nrd_min); });

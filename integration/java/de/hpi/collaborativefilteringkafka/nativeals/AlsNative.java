@@ -52,6 +52,9 @@ public final class AlsNative {
     public static native byte[] commUniqueId();
     /** als_comm_init: this engine becomes rank `rank` of `world`. */
     public static native void commInit(long engine, int world, int rank, byte[] uniqueId);
+    /** als_comm_set_timeout: bound on every wait for this engine's exchanges (ms); past it the communicator is
+     *  aborted and the waiting call throws, naming the pending all-gather. */
+    public static native void commSetTimeout(long engine, long timeoutMs);
     /** als_allgather_shard: chunk `chunk` of the side's chunk-major slots (unchunked: slotsPerShard, 0). */
     public static native void allgatherShard(long engine, int side, long slotsPerChunk, long chunk);
     /** als_predict: out[u * movieRows.length + m] = U[userRows[u]] . M[movieRows[m]] as a Java float dot. */

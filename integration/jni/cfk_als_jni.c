@@ -224,6 +224,12 @@ JNIEXPORT void JNICALL Java_de_hpi_collaborativefilteringkafka_nativeals_AlsNati
         fail_status(env, "als_comm_init", als_comm_init(ENGINE(engine), world, rank, buf));
 }
 
+JNIEXPORT void JNICALL Java_de_hpi_collaborativefilteringkafka_nativeals_AlsNative_commSetTimeout(
+        JNIEnv* env, jclass cls, jlong engine, jlong timeout_ms) {
+    (void)cls;
+    fail_status(env, "als_comm_set_timeout", als_comm_set_timeout(ENGINE(engine), (int64_t)timeout_ms));
+}
+
 JNIEXPORT void JNICALL Java_de_hpi_collaborativefilteringkafka_nativeals_AlsNative_allgatherShard(
         JNIEnv* env, jclass cls, jlong engine, jint side, jlong slots_per_chunk, jlong chunk) {
     (void)cls;

@@ -42,7 +42,7 @@ NATIVES = {
     "writeFactors": (None, [_i64, _i, _i64, _v, _i]), "readFactors": (None, [_i64, _i, _i64, _v, _i]),
     "writeFactorsF64": (None, [_i64, _i, _i64, _v, _i]), "readFactorsF64": (None, [_i64, _i, _i64, _v, _i]),
     "solveHalf": (None, [_i64, _i, _f]), "synchronize": (None, [_i64]), "commUniqueId": (_v, []),
-    "commInit": (None, [_i64, _i, _i, _v]), "allgatherShard": (None, [_i64, _i, _i64, _i64]),
+    "commInit": (None, [_i64, _i, _i, _v]), "commSetTimeout": (None, [_i64, _i64]), "allgatherShard": (None, [_i64, _i, _i64, _i64]),
     "predict": (None, [_i64, _v, _v, _v]), "writePredictionMatrixCsv": (None, [_v, _v, _i64, _i64]),
 }
 
@@ -156,6 +156,8 @@ def test_status_becomes_streams_exception_with_last_error(jvm):
     with pytest.raises(JavaException, match="num_features must be >= 1"):
         jvm.call("create", 0, 0, 0)
     jvm.call("destroy", 0)                            # als_engine_destroy(NULL) is a no-op, no exception
+    with pytest.raises(JavaException, match="als_comm_set_timeout: als_status 1"):
+        jvm.call("commSetTimeout", 0, 1000)           # NULL engine: ALS_ERR_INVALID_ARGUMENT
     assert jvm.stats()["violations"] == 0
 
 
