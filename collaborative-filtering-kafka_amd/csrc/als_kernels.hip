@@ -682,9 +682,13 @@ struct RowResidual {
 // DUAL: the system is the entry Gram of a short row (als_solve_dual): unknown 16b + j = the row's entry at
 // physical position 16b + j, real when that entry exists (padding entries get an identity row), and the
 // solution alpha goes to buf[16b + j] (read by the caller after a wave_sync) instead of a factor row.
+// u: the units of the tiles and the RHS -- the Gram terms are u^2 times the true ones and the RHS u times (the
+// pre-split Gram's table scale; 1 elsewhere). A' = D A D and D b do not depend on u (D scales by 1/u), so the
+// factorisation and the scaled solution are the same; the regularisation is added as lambda n u^2 and the solution
+// leaves in true units as D x' u.
 template <int C, bool DUAL = false, class TT, class KT>
 __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc)[C], float* buf, const Task& tk,
-                                            const SolveArgs& a, int lane) {
+                                            const SolveArgs& a, int lane, float u = 1.f) {
     const int g = lane >> 4, j = lane & 15;
     float* out = (float*)a.out + factor_row(a.row_offset, a.rows_per_chunk, a.chunk_stride, tk.row) * (int64_t)(16 * C);
     auto is_real = [&](int b) { return DUAL ? logical_entry(16 * b + j) < tk.nent : C * j + b < a.k; };
@@ -717,7 +721,7 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
     // get an identity row (their Gram rows/columns are exactly zero: padded factor columns are zero).
     // Then Jacobi scaling A' = D A D, b' = D b, x = D x' with D = diag(A)^{-1/2}: lane (g, j) of block b
     // needs s for column j (scol) and for rows 4g..4g+3 (srow), exchanged through buf.
-    const float reg = a.lambda * (float)tk.ndeg;
+    const float reg = a.lambda * (float)tk.ndeg * (u * u);
     const int jr = j & 3;
     const bool diag_lane = opaque(j >> 2) == g;   // lane holds a diagonal entry, in register j & 3
     float scol[C];
@@ -850,14 +854,14 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
     if (-1.f / nrd_min >= a.refine_min_pivot) {
         float xs[C];
 #pragma unroll
-        for (int b = 0; b < C; ++b) xs[b] = x[b] * scol[b];
+        for (int b = 0; b < C; ++b) xs[b] = x[b] * scol[b] * u;
         emit(xs);
         return;
     }
     if (a.flags & SOLVE_FLAG_SKIP_REFINE) {   // diagnostics only
         float xs[C];
 #pragma unroll
-        for (int b = 0; b < C; ++b) xs[b] = x[b] * scol[b];
+        for (int b = 0; b < C; ++b) xs[b] = x[b] * scol[b] * u;
         emit(xs);
         return;
     }
@@ -870,7 +874,7 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
         float z[C], acc[C];
 #pragma unroll
         for (int b = 0; b < C; ++b) {
-            z[b] = x[b] * scol[b];
+            z[b] = x[b] * scol[b] * u;   // true units
             acc[b] = 0.f;
         }
         using VT = typename VecC<C>::type;
@@ -897,7 +901,7 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
 #pragma unroll
         for (int b = 0; b < C; ++b) {
             const float gz = col_sum(acc[b]);
-            r[b] = b0[b] - (is_real(b) ? scol[b] * (gz + reg * z[b]) : x[b]);   // padded features: identity rows
+            r[b] = b0[b] - (is_real(b) ? scol[b] * u * (gz + reg * z[b]) : x[b]);   // padded features: identity rows
         }
     } else {
     wave_sync();
@@ -947,7 +951,7 @@ __device__ __forceinline__ void solve_tiles(TT& T, KT& A0, const float (&rhs_acc
     solve_vec(r, dx);
     float xs[C];
 #pragma unroll
-    for (int b = 0; b < C; ++b) xs[b] = (x[b] + dx[b]) * scol[b];
+    for (int b = 0; b < C; ++b) xs[b] = (x[b] + dx[b]) * scol[b] * u;
     emit(xs);
 }
 
@@ -1061,12 +1065,14 @@ __device__ __forceinline__ void store_partial(const SolveArgs& a, const Task& tk
 }
 
 // Pre-split fp16 Gram of one FULL / PARTIAL task into acc (tiles, RHS) and E (the diagonal tiles' h m^T terms,
-// folded by the caller), in true units. img: the wave's 2 C KB LDS image (1-KB aligned); buf: its KP floats.
+// folded by the caller), in the table's scaled units: Gram terms times 2^(2 sc), the RHS times 2^sc; returns sc.
+// The caller brings a PARTIAL task's sums back to true units for its slot and lets a FULL task's solve work in the
+// scaled ones (solve_tiles' u: the scaled system is the same after the Jacobi scaling), which saves the 72 ldexp of
+// the unscaling at KP = 64. img: the wave's 2 C KB LDS image (1-KB aligned); buf: its KP floats.
 template <int KP>
-__device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk, MfmaAcc<KP / 16>& acc,
-                                              f32x4 (&E)[KP / 16], unsigned char* img, float* buf, int lane) {
+__device__ __forceinline__ int gram_presplit(const SolveArgs& a, const Task& tk, MfmaAcc<KP / 16>& acc,
+                                             f32x4 (&E)[KP / 16], unsigned char* img, float* buf, int lane) {
     constexpr int C = KP / 16;
-    using Acc = MfmaAcc<C>;
     constexpr int B = BLOCK_SUBSTEPS;
     const int g = lane >> 4, j = lane & 15;
     const int nblk = (tk.nsteps + B - 1) / B;
@@ -1086,14 +1092,18 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
     for (int b = 0; b < C; ++b) racc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
     // the block's MFMAs on operands P[plane h/m][feature block b] (entries 8g..8g+7 of feature C j + b as
     // fp16 pairs) and the fp16 rating pairs R of the same entries (rh or rm by the lane's column)
-    auto mfma_block = [&](const u32x4 (&P)[NPL][C], const u32x4& R) {
+    // FIRST (the task's first block): every accumulator's first MFMA takes the inline constant 0 as its C operand,
+    // so the 72 zeroing moves of the accumulators (KP = 64) are not needed on this path
+    auto mfma_block = [&](const u32x4 (&P)[NPL][C], const u32x4& R, auto FIRST_) {
+        constexpr bool FIRST = decltype(FIRST_)::value;
+        const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int b1 = 0; b1 < C; ++b1)
 #pragma unroll
             for (int b2 = b1; b2 < C; ++b2) {
-                f32x4 t = acc.g[tile_index<C>(b1, b2)];
+                f32x4 t = FIRST ? zero : acc.g[tile_index<C>(b1, b2)];
                 if (b1 == b2) {
-                    E[b1] = mfma_f16(P[0][b1], P[1][b1], E[b1]);
+                    E[b1] = mfma_f16(P[0][b1], P[1][b1], FIRST ? zero : E[b1]);
                 } else {
                     t = mfma_f16(P[0][b1], P[1][b2], t);
                     t = mfma_f16(P[1][b1], P[0][b2], t);
@@ -1103,7 +1113,7 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
             }
 #pragma unroll
         for (int b = 0; b < C; ++b) {
-            f32x4 t = racc[b];
+            f32x4 t = FIRST ? zero : racc[b];
             t = mfma_f16(P[1][b], R, t);
             t = mfma_f16(P[0][b], R, t);
             racc[b] = t;
@@ -1179,7 +1189,7 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
         u32x4 Rn = rp[0];
         issue(cv);
         cv = cp[8 * min(1, lastb)];
-        for (int b = 0; b < nblk; ++b) {
+        auto step = [&](int b, auto FIRST_) {
             const u32x4 R = Rn;
             // every vector-memory op of this wave done: this block's LDS-DMA (and the column / rating loads
             // the DMA issue and the MFMAs below need anyway) -- explicit, not left to the compiler's tracking
@@ -1193,36 +1203,30 @@ __device__ __forceinline__ void gram_presplit(const SolveArgs& a, const Task& tk
             cv = cp[8 * min(b + 2, lastb)];
             Rn = rp[4 * min(b + 1, lastb)];
             __builtin_amdgcn_sched_barrier(0);
-            mfma_block(P, R);
+            mfma_block(P, R, FIRST_);
             __builtin_amdgcn_sched_barrier(0);
-        }
+        };
+        step(0, std::true_type{});
+        for (int b = 1; b < nblk; ++b) step(b, std::false_type{});
     }
-    // back to the table's units: the Gram terms by 2^-2sc, the RHS by 2^-sc (powers of two: exact)
-#pragma unroll
-    for (int t = 0; t < Acc::NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc.g[t][r] = ldexpf(acc.g[t][r], -2 * sc);
-#pragma unroll
-    for (int b = 0; b < C; ++b)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) E[b][r] = ldexpf(E[b][r], -2 * sc);
     // RHS tiles (row i of block b = feature C i + b; column 0 = Y^T rh, column 8 = Y^T rm) -> the per-lane
     // partial layout of the other paths: lane (0, j) holds feature C j + b, the other rows zero (col_sum
-    // restores it)
+    // restores it). The lane's (g, j) derived afresh (opaque): kept live across the Gram loop, one spilled.
+    const int lane2 = opaque(lane), g2 = lane2 >> 4, j2 = lane2 & 15;
     wave_sync();
 #pragma unroll
     for (int b = 0; b < C; ++b) {
         f32x4 v = racc[b];
 #pragma unroll
         for (int r = 0; r < 4; ++r)   // lane (g, 8) += lane (g, 0): DPP row_shr:8
-            v[r] = ldexpf(v[r] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[r]), 0x118,
-                                                                            0xf, 0xf, false)), -sc);
-        if (j == 8) *(f32x4*)(buf + 16 * b + 4 * g) = v;
+            v[r] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[r]), 0x118, 0xf, 0xf, false));
+        if (j2 == 8) *(f32x4*)(buf + 16 * b + 4 * g2) = v;
     }
     wave_sync();
 #pragma unroll
-    for (int b = 0; b < C; ++b) acc.rhs[b] = (g == 0) ? buf[16 * b + j] : 0.f;
+    for (int b = 0; b < C; ++b) acc.rhs[b] = (g2 == 0) ? buf[16 * b + j2] : 0.f;
     wave_sync();
+    return sc;
 }
 
 // REDUCE = true: the launch of a half's REDUCE tasks (sum of partial slots + solve), compiled apart from the
@@ -1270,6 +1274,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
 
         float* part = (float*)a.partials;
         constexpr int SLOT_WORDS = Acc::NWORDS + 1;   // + integrity check word
+        int ps_sc = 0;   // pre-split Gram: its sums are in units of 2^(2 ps_sc) (tiles) and 2^ps_sc (RHS)
         if constexpr (REDUCE) {
             // Fixed-order sum of the row's partial slots ([word][lane] layout, coalesced), each decoded and checked.
             bool bad = false;
@@ -1339,7 +1344,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
                 for (int c = 0; c < C; ++c) acc.rhs[c] += r * y[c];
             };
             if constexpr (PRESPLIT) {
-                gram_presplit<KP>(a, tk, acc, E, stage_lds[uni(wave)], buf, lane);
+                ps_sc = gram_presplit<KP>(a, tk, acc, E, stage_lds[uni(wave)], buf, lane);
             } else if constexpr (SPLIT) {
                 // Split-bf16 Gram: one v_mfma_f32_16x16x32_bf16 consumes a whole 32-entry block. Lane (g, j)
                 // holds A[i = j][k = 8g + t] = y_t[C*j + b] (its own gathered piece, component b, entry t of its
@@ -1625,11 +1630,30 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
 
         if constexpr (SPLIT && !REDUCE) {
             if constexpr (PRESPLIT)
-                fold_diag_lds<C>(acc, E, lane, stage_lds[uni(wave)]);   // the image is free after the Gram
+                // the image is free after the Gram; the fold's lane addresses are derived afresh (opaque: kept live
+                // across the Gram loop, one of them spilled at 128 VGPRs)
+                fold_diag_lds<C>(acc, E, opaque(lane), stage_lds[uni(wave)]);
             else
                 fold_diag<C>(acc, E, lane);
         }
 
+        // Pre-split units: a PARTIAL task's slot holds true units (the REDUCE launch sums slots unscaled); a FULL task
+        // solves in units of 2^keep (solve_tiles' u), keep = sc clamped to +-30 so that lambda n 2^(2 keep) stays a
+        // normal float (a table far from unit scale, rare, pays the ldexp of the difference). Powers of two: exact.
+        float u = 1.f;
+        if constexpr (PRESPLIT && !REDUCE) {
+            const int keep = tk.kind == TASK_PARTIAL ? 0 : min(max(ps_sc, -30), 30);
+            if (ps_sc != keep) {   // wave-uniform
+                const int d = ps_sc - keep;
+#pragma unroll
+                for (int p = 0; p < Acc::NT; ++p)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc.g[p][r] = ldexpf(acc.g[p][r], -2 * d);
+#pragma unroll
+                for (int c = 0; c < C; ++c) acc.rhs[c] = ldexpf(acc.rhs[c], -d);
+            }
+            u = ldexpf(1.f, keep);
+        }
         if (!REDUCE && tk.kind == TASK_PARTIAL) {
             store_partial<C>(a, tk, acc, lane);
             return;
@@ -1651,7 +1675,7 @@ __global__ __launch_bounds__(64 * mfma_waves<KP>(), MINW) void als_solve_mfma(So
         } else if constexpr (PRESPLIT && !REDUCE) {
             RegTiles<C> T{acc.g};
             RowResidual A0;
-            solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane);
+            solve_tiles<C>(T, A0, acc.rhs, buf, tk, a, lane, u);
         } else {
             RegTiles<C> T{acc.g};
             RegStore<C> A0;

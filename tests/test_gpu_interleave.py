@@ -116,3 +116,9 @@ def test_interleaved_plan_covers_every_entry_once(cfk):
     sw.solve_half(0, LAM)
     se, n = sw.sq_error(0)
     assert n == ds.nnz and np.isfinite(se)
+    # k = 128: a block whose long rows hold far fewer than 4 chunks of 16,384 entries per resident wave (every shard of
+    # the Netflix shape) takes the 4,096-entry chunk, capped by the contiguous chunk length
+    sw128 = _engine(cfk, blocks, 128, True)
+    i128 = sw128.split_info(0)
+    assert i128["chunk"] == min(4096, sw128.block_path(0)["chunk"]) and i128["interleaved_rows"] > 0, i128
+    assert i128["interleaved_rows"] == int((deg > i128["chunk"]).sum())
