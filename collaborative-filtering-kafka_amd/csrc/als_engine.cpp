@@ -116,6 +116,9 @@ struct als_engine {
     // ALS_INTERLEAVE: interleaved split rows + pre-split Gram for halves whose opposite table outgrows the L2s
     // (-1 auto, 0 off, 1 wherever the pre-split Gram exists)
     int interleave = -1;
+    // ALS_XCD_RANGES: an interleaved half's long rows are cut by opposite-slot range into 8 pieces whose chunks run on
+    // the XCD of that range (-1 auto: KP = 64 and an opposite table within 128 MiB, 0 off, 1 on)
+    int xcd_ranges = -1;
     uint32_t gen = 0;               // launch generation of the next PARTIAL/REDUCE pair
     int32_t debug_flags = 0;        // debug build only (CFK_DEBUG_KNOBS): ALS_DEBUG_SKIP_SOLVE / _REFINE
     uint32_t debug_gen_skew = 0;    // debug build only: ALS_DEBUG_REDUCE_GEN_SKEW=n, REDUCE decodes with generation
@@ -334,6 +337,7 @@ int als_engine_create(int device, int num_features, int precision, als_engine** 
     }
     if (const char* env = getenv("ALS_DUAL_SIDE")) e->dual_side = env[0] != '0';
     if (const char* env = getenv("ALS_INTERLEAVE")) e->interleave = env[0] == '0' ? 0 : 1;
+    if (const char* env = getenv("ALS_XCD_RANGES")) e->xcd_ranges = env[0] == '0' ? 0 : 1;
     if (const char* env = getenv("ALS_COMM_TIMEOUT_S")) e->comm_timeout_ms = (int64_t)(atof(env) * 1000.0);
     hipError_t st = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (st != hipSuccess) {
@@ -510,9 +514,34 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
     // (no longer than the contiguous chunk: a small block keeps enough tasks for load balance)
     const int64_t ilv = std::min(interleave_chunk(e, n_opp_rows, deg), chunk);
     std::vector<int32_t> perm;
+    std::vector<int8_t> srange;   // XCD range of each interleaved chunk task (ranges only)
     int64_t ilv_rows = 0;
+    // XCD ranges (ALS_XCD_RANGES): a long row's blocks are first grouped by the opposite slot of their first entry
+    // into X = 8 ranges of the opposite table (a row's entries ascend by slot, so each range is a run of its blocks),
+    // then each range's blocks are interleaved into chunks as below. Chunk tasks of range x all run on one XCD (the
+    // task order below), so that XCD's L2 serves 1/8 of the table instead of every XCD fetching all of it.
+    // Measured (profiles/r06c/ranges_*.log): the k = 64 Netflix-shape movie half (123 MB user table, one launch) 2.00
+    // -> 1.80 ms, iteration 4.73 -> 4.60 ms; the k = 128 movie half (246 MB) and the power-law shard's chunked item-table
+    // half (256 MB) a little slower, shards of G = 2 / 4 slower than their contiguous plan -- so auto = KP = 64 with an
+    // opposite table within 128 MiB (each XCD's range within 16 MiB).
+    constexpr int XR = 8;
+    const bool ranges = ilv > 0 && n_opp_rows > 0 &&
+                        (e->xcd_ranges > 0 ||
+                         (e->xcd_ranges < 0 && e->kp == 64 &&
+                          (n_opp_rows + 1) * (int64_t)cfk::presplit_row_bytes(e->kp) <= (128ll << 20)));
+    std::vector<int32_t> bfirst;   // opposite slot of every block's first entry (physical position 0 of the block)
+    if (ranges && nnz_padded > 0) {
+        bfirst.resize((size_t)(nnz_padded / cfk::BLOCK_ENTRIES));
+        hipError_t st = hipMemcpy2D(bfirst.data(), 4, d_col, cfk::BLOCK_ENTRIES * 4, 4, bfirst.size(),
+                                    hipMemcpyDeviceToHost);
+        if (st != hipSuccess) {
+            drop();
+            return fail(ALS_ERR_DEVICE, "set_block: block heads: %s", hipGetErrorString(st));
+        }
+    }
     if (ilv > 0) {
         constexpr int64_t BE = cfk::BLOCK_ENTRIES;
+        std::vector<int64_t> piece[XR];
         for (int64_t i = 0; i < n_rows; ++i) {
             const int64_t d = deg[i];
             if (d <= ilv) continue;
@@ -521,25 +550,43 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
                 for (size_t q = 0; q < perm.size(); ++q) perm[q] = (int32_t)q;
             }
             ++ilv_rows;
-            const int64_t nb = (d + BE - 1) / BE, nc = (d + ilv - 1) / ilv, b0 = begin[i] / BE;
+            const int64_t nb = (d + BE - 1) / BE, b0 = begin[i] / BE;
+            for (auto& v : piece) v.clear();
+            for (int64_t q = 0; q < nb; ++q) {
+                const int x = ranges ? (int)std::min<int64_t>(XR - 1, (int64_t)bfirst[(size_t)(b0 + q)] * XR / n_opp_rows)
+                                     : 0;
+                piece[x].push_back(q);
+            }
             Task t{};
             t.row = (int32_t)i;
             t.ndeg = (int32_t)d;
             t.kind = cfk::TASK_PARTIAL;
             const int64_t first = slots;
             int64_t pos = 0;
-            for (int64_t c = 0; c < nc; ++c) {
-                const int64_t p0 = pos;
-                for (int64_t x = c; x < nb; x += nc) perm[(size_t)(b0 + pos++)] = (int32_t)(b0 + x);
-                const int64_t cnt = pos - p0;
-                const bool last = (nb - 1) % nc == c;
-                const int64_t nent = last ? BE * (cnt - 1) + (d - BE * (nb - 1)) : BE * cnt;
-                Task p = t;
-                p.begin = begin[i] + BE * p0;
-                p.nent = (int32_t)nent;
-                p.nsteps = (int32_t)((nent + 3) / 4);
-                p.slot = (int32_t)slots++;
-                stasks.push_back(p);
+            for (int x = 0; x < XR; ++x) {
+                const std::vector<int64_t>& pb = piece[x];
+                if (pb.empty()) continue;
+                const int64_t np = (int64_t)pb.size();
+                const bool has_last = pb.back() == nb - 1;   // the row's padded block: last of its chunk below
+                const int64_t pent = BE * np - (has_last ? BE * nb - d : 0);
+                const int64_t nc = (pent + ilv - 1) / ilv;
+                for (int64_t c = 0; c < nc; ++c) {
+                    const int64_t p0 = pos;
+                    bool last = false;
+                    for (int64_t y = c; y < np; y += nc) {
+                        perm[(size_t)(b0 + pos++)] = (int32_t)(b0 + pb[(size_t)y]);
+                        last = pb[(size_t)y] == nb - 1;
+                    }
+                    const int64_t cnt = pos - p0;
+                    const int64_t nent = last ? BE * (cnt - 1) + (d - BE * (nb - 1)) : BE * cnt;
+                    Task p = t;
+                    p.begin = begin[i] + BE * p0;
+                    p.nent = (int32_t)nent;
+                    p.nsteps = (int32_t)((nent + 3) / 4);
+                    p.slot = (int32_t)slots++;
+                    stasks.push_back(p);
+                    srange.push_back((int8_t)x);
+                }
             }
             Task r = t;
             r.begin = 0;
@@ -646,7 +693,44 @@ int finish_block(als_engine* e, int side, int64_t n_rows, int64_t row_offset, in
         std::stable_sort(d.begin(), d.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
 
     // the interleaved chunks join the plain tasks, longest first
-    if (!stasks.empty()) {
+    if (!stasks.empty() && ranges) {
+        // XCD ranges: workgroup w runs on the XCD of w % 8 (round-robin placement; speed only, never correctness), so
+        // the workgroups at positions w = 8 j + x take range x's chunk tasks (queue x). The plain (whole-row) tasks have
+        // no range: each goes, longest first, to the queue of least work among those still short of an equal share of
+        // the task count, so the queues stay aligned to the round-robin. Every queue is longest first.
+        std::vector<Task> q[XR];
+        int64_t work[XR] = {};
+        for (size_t t = 0; t < stasks.size(); ++t) {
+            q[srange[t]].push_back(stasks[t]);
+            work[srange[t]] += stasks[t].nsteps;
+        }
+        const int64_t total = (int64_t)(stasks.size() + tasks.size());
+        const int64_t wgs = (total + 3) / 4;
+        for (const Task& t : tasks) {   // already longest first
+            int best = -1;
+            for (int x = 0; x < XR; ++x) {
+                const int64_t cap = 4 * ((wgs - x + XR - 1) / XR);   // tasks of the workgroups at w = x mod 8
+                if ((int64_t)q[x].size() < cap && (best < 0 || work[x] < work[best])) best = x;
+            }
+            if (best < 0) best = (int)(std::min_element(work, work + XR) - work);
+            q[best].push_back(t);
+            work[best] += t.nsteps;
+        }
+        std::vector<Task> out;
+        out.reserve((size_t)total);
+        for (int x = 0; x < XR; ++x)
+            std::stable_sort(q[x].begin(), q[x].end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
+        for (size_t j = 0;; j += 4) {
+            bool any = false;
+            for (int x = 0; x < XR; ++x)
+                for (size_t u = j; u < j + 4 && u < q[x].size(); ++u) {
+                    out.push_back(q[x][u]);
+                    any = true;
+                }
+            if (!any) break;
+        }
+        tasks.swap(out);
+    } else if (!stasks.empty()) {
         tasks.insert(tasks.begin(), stasks.begin(), stasks.end());
         std::stable_sort(tasks.begin(), tasks.end(), [](const Task& a, const Task& b) { return a.nsteps > b.nsteps; });
     }

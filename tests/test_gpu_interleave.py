@@ -24,16 +24,18 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-def _engine(cfk, blocks, k, ilv):
-    old = os.environ.get("ALS_INTERLEAVE")
+def _engine(cfk, blocks, k, ilv, ranges=False):
+    saved = {v: os.environ.get(v) for v in ("ALS_INTERLEAVE", "ALS_XCD_RANGES")}
     os.environ["ALS_INTERLEAVE"] = "1" if ilv else "0"
+    os.environ["ALS_XCD_RANGES"] = "1" if ranges else "0"
     try:
         eng = cfk.ALSEngine(k, "f32")
     finally:
-        if old is None:
-            del os.environ["ALS_INTERLEAVE"]
-        else:
-            os.environ["ALS_INTERLEAVE"] = old
+        for v, old in saved.items():
+            if old is None:
+                del os.environ[v]
+            else:
+                os.environ[v] = old
     eng.use_torch_stream()
     eng.alloc_factors(0, blocks[0]["n_slots"])
     eng.alloc_factors(1, blocks[1]["n_slots"])
@@ -122,3 +124,41 @@ def test_interleaved_plan_covers_every_entry_once(cfk):
     i128 = sw128.split_info(0)
     assert i128["chunk"] == min(4096, sw128.block_path(0)["chunk"]) and i128["interleaved_rows"] > 0, i128
     assert i128["interleaved_rows"] == int((deg > i128["chunk"]).sum())
+
+
+@pytest.mark.timeout(300)
+def test_xcd_range_pieces_cover_every_entry_and_match_the_oracle(cfk, oracle_mod):
+    """ALS_XCD_RANGES: each long row cut into 8 opposite-slot ranges before the interleave, the
+    chunks of range x ordered onto the workgroups of one XCD. Same arithmetic per chunk, another summation order: every
+    entry in exactly one task, one REDUCE per long row, at least one chunk per range a row reaches, results against the
+    fp64 oracle within 3x the plain interleaved plan's error, bitwise repeat, clean integrity record."""
+    from test_gpu_fullscale import _check_rows
+    ds = cfk.Dataset.synthetic_netflix(30_000, 1_000, 6_000_000, seed=0xA16, nthreads=16)
+    blocks = [ds.shard_block(0), ds.shard_block(1)]
+    k = 64
+    rg = _engine(cfk, blocks, k, True, ranges=True)
+    sw = _engine(cfk, blocks, k, True)
+    deg = np.diff(blocks[0]["row_ptr"])
+    i_rg, i_sw = rg.split_info(0), sw.split_info(0)
+    assert i_rg["interleaved_rows"] == i_sw["interleaved_rows"] == int((deg > i_rg["chunk"]).sum()) > 0
+    assert i_rg["chunk_tasks"] >= i_sw["chunk_tasks"]
+    assert rg.block_stats(0)["n_reduce"] == i_rg["interleaved_rows"]
+    u0 = ds.init_user_factors(k, 42)
+    for e in (rg, sw):
+        e.write_factors(1, u0)
+        e.solve_half(0, LAM)
+    m_rg, m_sw = rg.read_factors(0), sw.read_factors(0)
+    assert rg.integrity_status() == [0, 0, 0, 0]
+    rng = np.random.default_rng(7)
+    rows = np.unique(np.concatenate([np.argsort(-deg)[:20], rng.choice(len(deg), 100, replace=False)]))
+    e_rg = _check_rows(oracle_mod, blocks[0], rows, m_rg, u0.astype(np.float64), "XCD-range movie half")
+    e_sw = _check_rows(oracle_mod, blocks[0], rows, m_sw, u0.astype(np.float64), "interleaved movie half")
+    assert e_rg <= 3 * max(e_sw, 1e-7), (e_rg, e_sw)
+    rg.write_factors(1, u0)
+    rg.solve_half(0, LAM)
+    assert np.array_equal(rg.read_factors(0), m_rg)
+    rg.write_factors(0, m_sw)
+    se_rg, n_rg = rg.sq_error(0)
+    sw.write_factors(0, m_sw)
+    se_sw, n_sw = sw.sq_error(0)
+    assert n_rg == n_sw == ds.nnz and abs(se_rg - se_sw) <= 1e-10 * se_sw, (se_rg, se_sw)
