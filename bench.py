@@ -521,6 +521,9 @@ def main():
                        "launches_per_half": {"movie": app.info[0]["n_chunks"], "user": app.info[1]["n_chunks"]}},
             "solves_per_s": ((info["movie"]["n_rows"] + info["user"]["n_rows"]) if solo else (nm + nu)) * K / elapsed,
             "projected_job_ratings_per_s_compute_only": value * args.shard_of if solo else None,
+            "projection_note": ("this rank's rate x G: assumes balanced shards (id % G balances the Netflix shape; on the "
+                                "power-law workload the heaviest items make rank 0 the longest) and leaves out the "
+                                "exchange (DESIGN.md section 4)") if solo else None,
             "mse_after": mse,
             "replicas_agree": check["replicas_agree"], "integrity_clean": check["integrity_clean"],
             "replica_digest": check["digest"],
