@@ -484,7 +484,10 @@ int64_t interleave_chunk(const als_engine* e, int64_t n_opp_rows, const std::vec
     int64_t len;
     if (e->kp == 64) {
         len = 10240;
-        if (e->interleave < 0 && long_work(len) < len * conc * 3 / 2) return 0;
+        // the concurrency rule holds for the 123 MB user table of a Netflix shard; the 256 MB item table of the
+        // power-law shard's user half interleaves whatever its long-row work (9.43 -> 7.38 ms, profiles/r06a; the rule
+        // alone had turned it off again: 9.47-9.57 ms, profiles/r06c/ranges_bench_ab)
+        if (e->interleave < 0 && sb <= (128ll << 20) && long_work(len) < len * conc * 3 / 2) return 0;
     } else {
         len = long_work(16384) >= 16384 * 4 * conc ? 16384 : 4096;
     }
