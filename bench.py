@@ -42,9 +42,13 @@ FP32_PEAK_TFS = 157.3        # f32 vector = f32 MFMA dense peak
 MFMA16_PEAK_TFS = 2500.0     # dense bf16 / f16 MFMA peak (no sparsity; the f16 forms take the bf16 cycles)
 # MI355X_MICROARCH.md "Indexed rows: gather into LDS": uniformly random rows of a 151 MB table (the 123 MB k = 64
 # user table the movie half gathers sits between its 38 MB and 151 MB rows) are served at 7.4-7.9 TB/s chip-wide;
-# rows every workgroup shares from the XCD's L2 (the 4.5 MB pre-split movie table of the user half) at 16.8-18.8 TB/s
+# rows every workgroup shares from the XCD's L2 at 16.8-18.8 TB/s there. This repository's own gather microbenchmark
+# (tools/gather_bench.hip: 256-B rows in 8-KB blocks, 16 waves per CU, nothing else running) moves uniformly random rows
+# of the 4.5 MB pre-split movie table at 22.0-22.2 TB/s (profiles/r05e/gather_bench.log, profiles/r06c/
+# gather_bench_*.log; 25 TB/s with the Netflix popularity skew) and of a 123 MB table at 7.1-7.6 TB/s: the L2 ceiling is
+# the higher measured uniform-row rate, so the fraction is not flattered by the guide's lower figure.
 IC_GATHER_CEILING_GBS = 7900.0
-L2_GATHER_CEILING_GBS = 18800.0
+L2_GATHER_CEILING_GBS = 22200.0
 L2_RESIDENT_BYTES = 8 << 20  # a gathered table this small stays in every XCD's 4 MiB L2 to most of its rows
 IC_RESIDENT_BYTES = 256 << 20   # Infinity Cache: a larger gathered table streams from HBM (configs[4]'s 2.56 GB U)
 MFMA_FLOP = 16 * 16 * 32 * 2   # one v_mfma_f32_16x16x32_{bf16,f16}
